@@ -1,0 +1,595 @@
+// Chunk root (DeriveSha over body bytes) on gfx950 — see chunk_root.h for the design.
+//
+// Restated semantics:
+//   core/types/derive_sha.go:32-41   key_i = rlp(uint(i)), value_i = Chunks.GetRlp(i) = rlp(body[i])
+//   trie/trie.go:218-286             insert: short (leaf/extension) and full (branch) nodes
+//   trie/hasher.go:56-212            post-order hashing, RLP < 32 bytes inlined, root forced
+//   trie/encoding.go:37-75           hexToCompact (flag 2 = leaf, +1 odd) and keybytesToHex
+//   trie/trie.go:471-478             empty trie -> emptyRoot (handled by the host)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "chunk_root.h"
+#include "gsv_internal.h"
+#include "keccak_dev.cuh"
+
+namespace gsv {
+
+// ================================================================ key helpers (host + device)
+// nibbles of keybytesToHex(rlp(uint(i))) including the terminator 16
+__host__ __device__ inline int key_nbytes(uint32_t i) {
+    return i < 128 ? 1 : i < 256 ? 2 : i < 65536 ? 3 : 4;  // i == 0 -> [0x80] (1 byte)
+}
+__host__ __device__ inline uint8_t key_byte(uint32_t i, int b) {
+    int nb = key_nbytes(i);
+    if (nb == 1) return i == 0 ? 0x80 : (uint8_t)i;
+    if (b == 0) return (uint8_t)(0x80 + nb - 1);
+    return (uint8_t)(i >> (8 * (nb - 1 - b)));
+}
+__host__ __device__ inline int key_len(uint32_t i) { return 2 * key_nbytes(i) + 1; }
+__host__ __device__ inline uint8_t key_nib(uint32_t i, int d) {
+    int nb = key_nbytes(i);
+    if (d >= 2 * nb) return 16;
+    uint8_t by = key_byte(i, d >> 1);
+    return (d & 1) ? (by & 15) : (by >> 4);
+}
+
+// ================================================================ host plan builder
+namespace {
+
+struct Builder {
+    uint32_t N;
+    uint32_t nB;  // keys 1..127 present (they sort first)
+    std::vector<PNode> nodes;
+    std::vector<std::vector<PChild>> kids;
+
+    uint32_t ipos(uint32_t p) const {
+        if (p < nB) return 1 + p;
+        p -= nB;
+        return p == 0 ? 0u : 127u + p;
+    }
+
+    struct Res {
+        bool leaf;
+        uint32_t i;      // leaf body index
+        uint16_t depth;  // leaf remainder start
+        int node;        // node id
+        int height;
+    };
+
+    int new_node(uint8_t kind) {
+        PNode n{};
+        n.kind = kind;
+        n.msg_off = -1;
+        n.parent_msg = -1;
+        n.ref_slot = -1;
+        n.child_begin = -1;
+        nodes.push_back(n);
+        kids.emplace_back();
+        return (int)nodes.size() - 1;
+    }
+
+    Res build(uint32_t lo, uint32_t hi, int depth) {
+        if (hi - lo == 1) return Res{true, ipos(lo), (uint16_t)depth, -1, 0};
+        uint32_t fi = ipos(lo), la = ipos(hi - 1);
+        int cp = depth;
+        while (key_nib(fi, cp) == key_nib(la, cp)) cp++;
+        if (cp > depth) {
+            Res c = build(lo, hi, cp);
+            int id = new_node(PK_EXT);
+            nodes[id].first_i = fi;
+            nodes[id].depth = (uint16_t)depth;
+            nodes[id].ext_end = (uint16_t)cp;
+            nodes[id].height = (uint8_t)(c.height + 1);
+            kids[id].push_back(PChild{0, PC_NODE, 0, (uint32_t)c.node});
+            return Res{false, 0, 0, id, c.height + 1};
+        }
+        // branch at `depth`: partition [lo, hi) by nibble (monotone in sorted order)
+        uint32_t starts[17];
+        uint8_t vals[16];
+        int nch = 0;
+        uint32_t s = lo;
+        while (s < hi) {
+            uint8_t v = key_nib(ipos(s), depth);
+            uint32_t a = s + 1, b = hi;  // first position with nibble > v
+            while (a < b) {
+                uint32_t m = a + (b - a) / 2;
+                if (key_nib(ipos(m), depth) > v) b = m;
+                else a = m + 1;
+            }
+            starts[nch] = s;
+            vals[nch] = v;
+            nch++;
+            s = a;
+        }
+        starts[nch] = hi;
+        // full bottom branch: 16 single keys whose remainder after this nibble is the terminator
+        if (nch == 16 && hi - lo == 16) {
+            bool bottom = true;
+            for (uint32_t p = lo; p < hi && bottom; p++) bottom = key_len(ipos(p)) - 1 == depth + 1;
+            if (bottom) {
+                int id = new_node(PK_BOTTOM);
+                nodes[id].first_i = fi;
+                nodes[id].depth = (uint16_t)depth;
+                nodes[id].height = 1;
+                return Res{false, 0, 0, id, 1};
+            }
+        }
+        std::vector<PChild> ch;
+        int h = 0;
+        bool all_hashed_full = (nch == 16);
+        for (int c = 0; c < nch; c++) {
+            Res r = build(starts[c], starts[c + 1], depth + 1);
+            if (r.leaf) {
+                ch.push_back(PChild{vals[c], PC_LEAF, r.depth, r.i});
+                all_hashed_full = false;
+            } else {
+                ch.push_back(PChild{vals[c], PC_NODE, 0, (uint32_t)r.node});
+                uint8_t k = nodes[r.node].kind;
+                if (k != PK_BOTTOM && k != PK_HFULL) all_hashed_full = false;
+            }
+            h = std::max(h, r.height);
+        }
+        int id = new_node(all_hashed_full ? PK_HFULL : PK_BRANCH);
+        nodes[id].first_i = fi;
+        nodes[id].depth = (uint16_t)depth;
+        nodes[id].height = (uint8_t)(h + 1);
+        kids[id] = std::move(ch);
+        return Res{false, 0, 0, id, h + 1};
+    }
+};
+
+}  // namespace
+
+void build_trie_plan(TriePlanHost& p, uint32_t N) {
+    p = TriePlanHost();
+    p.N = N;
+    if (N == 0) return;
+    Builder b;
+    b.N = N;
+    b.nB = N > 128 ? 127 : N - 1;
+    Builder::Res r = b.build(0, N, 0);
+    int root;
+    if (r.leaf) {  // N == 1: a single leaf is the root
+        root = b.new_node(PK_LEAF);
+        b.nodes[root].first_i = r.i;
+        b.nodes[root].depth = r.depth;
+        b.nodes[root].height = 1;
+    } else {
+        root = r.node;
+    }
+    b.nodes[root].is_root = 1;
+    // an HFULL root still has to produce the root hash (no parent message): fine, handled in-kernel
+    // order: by height, BOTTOM first at height 1
+    int M = (int)b.nodes.size();
+    std::vector<int> order(M);
+    for (int i = 0; i < M; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        const PNode &a = b.nodes[x], &c = b.nodes[y];
+        if (a.height != c.height) return a.height < c.height;
+        return (a.kind == PK_BOTTOM) > (c.kind == PK_BOTTOM);
+    });
+    std::vector<int> newid(M);
+    for (int i = 0; i < M; i++) newid[order[i]] = i;
+    p.nodes.resize(M);
+    int nmsg = 0;
+    for (int i = 0; i < M; i++) {
+        int o = order[i];
+        PNode n = b.nodes[o];
+        n.ref_slot = i;
+        if (n.kind != PK_BOTTOM) n.msg_off = (nmsg++) * MSG_STRIDE;
+        const auto& kv = b.kids[o];
+        if (!kv.empty() && n.kind != PK_HFULL) {
+            n.child_begin = (int)p.children.size();
+            n.nchild = (uint8_t)kv.size();
+            for (auto c : kv) {
+                if (c.type == PC_NODE) c.idx = (uint32_t)newid[c.idx];
+                p.children.push_back(c);
+            }
+        }
+        p.nodes[i] = n;
+    }
+    // HFULL parents: children write "a0 || hash" at 3 + 33 * slot of the parent's message
+    for (int i = 0; i < M; i++) {
+        int o = order[i];
+        if (b.nodes[o].kind != PK_HFULL) continue;
+        for (auto& c : b.kids[o]) p.nodes[newid[c.idx]].parent_msg = p.nodes[i].msg_off + 3 + 33 * c.slot;
+    }
+    p.root = newid[root];
+    p.n_msg = nmsg;
+    p.n_slots = M;
+    p.height = p.nodes.back().height;
+    for (int h = 1; h <= p.height; h++) {
+        int bb = -1, be = -1, gb = -1, ge = -1;
+        for (int i = 0; i < M; i++) {
+            if (p.nodes[i].height != h) continue;
+            if (p.nodes[i].kind == PK_BOTTOM) {
+                if (bb < 0) bb = i;
+                be = i + 1;
+            } else {
+                if (gb < 0) gb = i;
+                ge = i + 1;
+            }
+        }
+        p.lvl_bottom_begin.push_back(bb < 0 ? 0 : bb);
+        p.lvl_bottom_end.push_back(bb < 0 ? 0 : be);
+        p.lvl_gen_begin.push_back(gb < 0 ? 0 : gb);
+        p.lvl_gen_end.push_back(gb < 0 ? 0 : ge);
+    }
+}
+
+PlanCache::~PlanCache() {
+    for (auto& kv : plans_) {
+        if (kv.second->d_nodes) (void)hipFree(kv.second->d_nodes);
+        if (kv.second->d_children) (void)hipFree(kv.second->d_children);
+    }
+}
+
+TriePlan* PlanCache::get(uint32_t N) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = plans_.find(N);
+    if (it != plans_.end()) return it->second.get();
+    auto pl = std::make_unique<TriePlan>();
+    build_trie_plan(pl->h, N);
+    if (!pl->h.nodes.empty()) {
+        if (hipMalloc(&pl->d_nodes, pl->h.nodes.size() * sizeof(PNode)) != hipSuccess) return nullptr;
+        if (hipMemcpy(pl->d_nodes, pl->h.nodes.data(), pl->h.nodes.size() * sizeof(PNode),
+                      hipMemcpyHostToDevice) != hipSuccess)
+            return nullptr;
+        if (!pl->h.children.empty()) {
+            if (hipMalloc(&pl->d_children, pl->h.children.size() * sizeof(PChild)) != hipSuccess) return nullptr;
+            if (hipMemcpy(pl->d_children, pl->h.children.data(), pl->h.children.size() * sizeof(PChild),
+                          hipMemcpyHostToDevice) != hipSuccess)
+                return nullptr;
+        }
+    }
+    TriePlan* r = pl.get();
+    plans_[N] = std::move(pl);
+    return r;
+}
+
+// ================================================================ device side
+struct BodyBatch {
+    const uint8_t* bodies;     // base of all bodies
+    const uint64_t* body_off;  // per body start offset (device)
+    uint8_t* msg;              // msg arena base; body b at msg + b * msg_stride
+    uint8_t* refs;             // ref arena base; body b at refs + b * ref_stride
+    uint8_t* roots;            // 32 B per body
+    uint64_t msg_stride, ref_stride;
+    uint32_t nbodies;
+};
+
+// Keccak-256 of len bytes at p (8-byte aligned; bytes past len may be garbage)
+GSV_DI void keccak_buf(uint32_t h[8], const uint8_t* p, uint32_t len) {
+    uint64_t a[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) a[k] = 0;
+    const uint64_t* q = (const uint64_t*)p;
+    while (len >= 136) {
+#pragma unroll
+        for (int k = 0; k < 17; k++) a[k] ^= q[k];
+        keccakf(a);
+        q += 17;
+        len -= 136;
+    }
+#pragma unroll
+    for (int k = 0; k < 17; k++) {
+        int32_t avail = (int32_t)len - 8 * k;
+        uint64_t w = 0;
+        if (avail >= 8) w = q[k];
+        else if (avail > 0) w = q[k] & ((1ull << (8 * avail)) - 1ull);
+        if ((uint32_t)(len >> 3) == (uint32_t)k) w ^= 0x01ull << (8 * (len & 7u));
+        if (k == 16) w ^= 0x8000000000000000ULL;
+        a[k] ^= w;
+    }
+    keccakf(a);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        h[2 * k] = (uint32_t)a[k];
+        h[2 * k + 1] = (uint32_t)(a[k] >> 32);
+    }
+}
+
+// write "a0 || hash" (33 bytes) at dst, byte granular
+GSV_DI void put_hashref(uint8_t* dst, const uint32_t h[8]) {
+    dst[0] = 0xa0;
+#pragma unroll
+    for (int w = 0; w < 8; w++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) dst[1 + 4 * w + b] = (uint8_t)(h[w] >> (8 * b));
+}
+
+// deliver a hashed node's reference (root output / parent message / canonical slot)
+GSV_DI void emit_hash(const PNode& nd, const BodyBatch& bb, uint32_t body, const uint32_t h[8]) {
+    if (nd.is_root) {
+        uint8_t* o = bb.roots + (size_t)body * 32;
+#pragma unroll
+        for (int w = 0; w < 8; w++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) o[4 * w + b] = (uint8_t)(h[w] >> (8 * b));
+    } else if (nd.parent_msg >= 0) {
+        put_hashref(bb.msg + (size_t)body * bb.msg_stride + nd.parent_msg, h);
+    } else {
+        uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE;
+        s[0] = 33;
+        put_hashref(s + 8, h);
+    }
+}
+
+// ---------------------------------------------------------------- BOTTOM: 16 leaf children
+// leaf j = [0x20, rlp(b)]: b == 0 -> c3 20 81 80; b < 128 -> c2 20 b; else c4 20 82 81 b
+constexpr int BOT_BLOCK = 256;
+constexpr int BOT_BUF = 96;
+
+__global__ __launch_bounds__(BOT_BLOCK) void k_chunk_bottom(const PNode* __restrict__ nodes, int nb0,
+                                                            int ncount, BodyBatch bb) {
+    __shared__ uint64_t sbuf64[BOT_BLOCK * BOT_BUF / 8];
+    uint64_t t = (uint64_t)blockIdx.x * BOT_BLOCK + threadIdx.x;
+    if (t >= (uint64_t)ncount * bb.nbodies) return;
+    uint32_t body = (uint32_t)(t / (uint64_t)ncount);
+    int ni = nb0 + (int)(t % (uint64_t)ncount);
+    const PNode nd = nodes[ni];
+    const uint8_t* src = bb.bodies + bb.body_off[body] + nd.first_i;
+    uint8_t v[16];
+    if ((((uintptr_t)src) & 15u) == 0) {
+        uint4 w = *(const uint4*)src;
+        uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = (uint8_t)(ws[j >> 2] >> (8 * (j & 3)));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = src[j];
+    }
+    uint32_t payload = 1;  // trailing empty value slot 0x80
+#pragma unroll
+    for (int j = 0; j < 16; j++) payload += v[j] == 0 ? 4u : v[j] < 128 ? 3u : 5u;
+    uint8_t* m = (uint8_t*)sbuf64 + threadIdx.x * BOT_BUF;
+    uint32_t o = 0;
+    if (payload < 56) {
+        m[o++] = (uint8_t)(0xc0 + payload);
+    } else {
+        m[o++] = 0xf8;
+        m[o++] = (uint8_t)payload;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint8_t b = v[j];
+        if (b == 0) {
+            m[o] = 0xc3; m[o + 1] = 0x20; m[o + 2] = 0x81; m[o + 3] = 0x80;
+            o += 4;
+        } else if (b < 128) {
+            m[o] = 0xc2; m[o + 1] = 0x20; m[o + 2] = b;
+            o += 3;
+        } else {
+            m[o] = 0xc4; m[o + 1] = 0x20; m[o + 2] = 0x82; m[o + 3] = 0x81; m[o + 4] = b;
+            o += 5;
+        }
+    }
+    m[o++] = 0x80;
+    // zero the rest of the 88-byte window, then pad (single block: len <= 83 < 136)
+    for (uint32_t k = o; k < 88; k++) m[k] = 0;
+    uint64_t a[25];
+    const uint64_t* q = (const uint64_t*)m;
+#pragma unroll
+    for (int k = 0; k < 11; k++) a[k] = q[k];
+#pragma unroll
+    for (int k = 11; k < 25; k++) a[k] = 0;
+    // 0x01 at byte o (o <= 83 -> lane <= 10)
+    uint32_t lane = o >> 3;
+#pragma unroll
+    for (int k = 0; k < 11; k++)
+        if ((uint32_t)k == lane) a[k] ^= 0x01ull << (8 * (o & 7u));
+    a[16] ^= 0x8000000000000000ULL;
+    keccakf(a);
+    uint32_t h[8];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        h[2 * k] = (uint32_t)a[k];
+        h[2 * k + 1] = (uint32_t)(a[k] >> 32);
+    }
+    emit_hash(nd, bb, body, h);
+}
+
+// ---------------------------------------------------------------- generic encoding helpers
+// compact encoding (trie/encoding.go:37-52) of nibbles key(i)[d0:d1] (terminator included iff
+// present); returns byte length, writes into c[0..]
+GSV_DI int compact_key(uint8_t c[8], uint32_t i, int d0, int d1) {
+    int term = (d1 > d0 && key_nib(i, d1 - 1) == 16) ? 1 : 0;
+    int hl = d1 - d0 - term;
+    int n = 1;
+    c[0] = (uint8_t)(term << 5);
+    int d = d0;
+    if (hl & 1) {
+        c[0] |= (uint8_t)(0x10 | key_nib(i, d));
+        d++;
+        hl--;
+    }
+    for (int k = 0; k < hl; k += 2) c[n++] = (uint8_t)((key_nib(i, d + k) << 4) | key_nib(i, d + k + 1));
+    return n;
+}
+
+struct Writer {
+    uint8_t* p;
+    uint32_t n;
+    bool dry;
+    GSV_DI void put(uint8_t b) {
+        if (!dry) p[n] = b;
+        n++;
+    }
+    GSV_DI void str(const uint8_t* s, int len) {  // RLP string
+        if (len == 1 && s[0] < 0x80) {
+            put(s[0]);
+            return;
+        }
+        put((uint8_t)(0x80 + len));  // len < 56 here
+        for (int k = 0; k < len; k++) put(s[k]);
+    }
+    GSV_DI void list_header(uint32_t len) {
+        if (len < 56) put((uint8_t)(0xc0 + len));
+        else if (len < 256) {
+            put(0xf8);
+            put((uint8_t)len);
+        } else {
+            put(0xf9);
+            put((uint8_t)(len >> 8));
+            put((uint8_t)len);
+        }
+    }
+};
+
+// leaf [compact(rem), rlp(value)] where value = rlp(uint(body byte))
+GSV_DI void write_leaf(Writer& w, uint32_t i, int d, uint8_t b) {
+    uint8_t ck[8];
+    int cl = compact_key(ck, i, d, key_len(i));
+    uint32_t klen = (cl == 1 && ck[0] < 0x80) ? 1u : 1u + cl;
+    uint32_t vlen = b == 0 ? 2u : b < 128 ? 1u : 3u;
+    w.list_header(klen + vlen);
+    w.str(ck, cl);
+    if (b == 0) {
+        w.put(0x81);
+        w.put(0x80);
+    } else if (b < 128) {
+        w.put(b);
+    } else {
+        w.put(0x82);
+        w.put(0x81);
+        w.put(b);
+    }
+}
+
+GSV_DI void write_child_ref(Writer& w, const BodyBatch& bb, uint32_t body, const PChild& c,
+                            const PNode* nodes) {
+    if (c.type == PC_LEAF) {
+        uint8_t b = bb.bodies[bb.body_off[body] + c.idx];
+        write_leaf(w, c.idx, c.depth, b);
+    } else {
+        const uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nodes[c.idx].ref_slot * REF_STRIDE;
+        uint32_t len = s[0];
+        for (uint32_t k = 0; k < len; k++) w.put(s[8 + k]);
+    }
+}
+
+// payload of a generic node into w
+GSV_DI void write_payload(Writer& w, const PNode& nd, const PChild* ch, const BodyBatch& bb,
+                          uint32_t body, const PNode* nodes) {
+    if (nd.kind == PK_BRANCH) {
+        int k = 0;
+        for (int slot = 0; slot < 16; slot++) {
+            if (k < nd.nchild && ch[k].slot == slot) {
+                write_child_ref(w, bb, body, ch[k], nodes);
+                k++;
+            } else {
+                w.put(0x80);
+            }
+        }
+        w.put(0x80);  // value slot (never set: keys are prefix-free)
+    } else if (nd.kind == PK_EXT) {
+        uint8_t ck[8];
+        int cl = compact_key(ck, nd.first_i, nd.depth, nd.ext_end);
+        w.str(ck, cl);
+        write_child_ref(w, bb, body, ch[0], nodes);
+    } else {  // PK_LEAF (root of a 1-byte body)
+        uint8_t b = bb.bodies[bb.body_off[body] + nd.first_i];
+        uint8_t ck[8];
+        int cl = compact_key(ck, nd.first_i, nd.depth, key_len(nd.first_i));
+        w.str(ck, cl);
+        if (b == 0) {
+            w.put(0x81);
+            w.put(0x80);
+        } else if (b < 128) {
+            w.put(b);
+        } else {
+            w.put(0x82);
+            w.put(0x81);
+            w.put(b);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ nodes,
+                                                     const PChild* __restrict__ children, int g0,
+                                                     int ncount, BodyBatch bb) {
+    uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (uint64_t)ncount * bb.nbodies) return;
+    uint32_t body = (uint32_t)(t / (uint64_t)ncount);
+    int ni = g0 + (int)(t % (uint64_t)ncount);
+    const PNode nd = nodes[ni];
+    uint8_t* m = bb.msg + (size_t)body * bb.msg_stride + nd.msg_off;
+    uint32_t h[8];
+    if (nd.kind == PK_HFULL) {
+        // children wrote bytes [3, 531); header f9 02 11, value slot 0x80 at 531
+        m[0] = 0xf9;
+        m[1] = 0x02;
+        m[2] = 0x11;
+        m[531] = 0x80;
+        keccak_buf(h, m, 532);
+        emit_hash(nd, bb, body, h);
+        return;
+    }
+    const PChild* ch = nd.child_begin >= 0 ? children + nd.child_begin : nullptr;
+    Writer dry{m, 0, true};
+    write_payload(dry, nd, ch, bb, body, nodes);
+    uint32_t plen = dry.n;
+    Writer w{m, 0, false};
+    w.list_header(plen);
+    write_payload(w, nd, ch, bb, body, nodes);
+    uint32_t len = w.n;
+    if (len >= 32 || nd.is_root) {
+        keccak_buf(h, m, len);
+        emit_hash(nd, bb, body, h);
+    } else {
+        // inline: the RLP itself is the reference (trie/hasher.go:163)
+        uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE;
+        s[0] = (uint8_t)len;
+        for (uint32_t k = 0; k < len; k++) s[8 + k] = m[k];
+    }
+}
+
+// ================================================================ launcher
+size_t chunk_root_scratch_bytes(const TriePlan* plan, uint32_t nbodies) {
+    size_t ms = (size_t)plan->h.n_msg * MSG_STRIDE;
+    size_t rs = (size_t)plan->h.n_slots * REF_STRIDE;
+    return (ms + rs) * nbodies + 512;
+}
+
+hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies, const uint64_t* d_body_off,
+                                  uint32_t nbodies, uint8_t* d_scratch, uint8_t* d_roots, hipStream_t st,
+                                  void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
+                                  void* tctx) {
+    const TriePlanHost& p = plan->h;
+    if (nbodies == 0 || p.nodes.empty()) return hipSuccess;
+    BodyBatch bb;
+    bb.bodies = d_bodies;
+    bb.body_off = d_body_off;
+    bb.msg_stride = (size_t)p.n_msg * MSG_STRIDE;
+    bb.ref_stride = (size_t)p.n_slots * REF_STRIDE;
+    bb.msg = d_scratch;
+    bb.refs = d_scratch + bb.msg_stride * nbodies;
+    bb.roots = d_roots;
+    bb.nbodies = nbodies;
+    for (int h = 1; h <= p.height; h++) {
+        int b0 = p.lvl_bottom_begin[h - 1], b1 = p.lvl_bottom_end[h - 1];
+        if (b1 > b0) {
+            uint64_t total = (uint64_t)(b1 - b0) * nbodies;
+            if (timer_begin) timer_begin(tctx, GSV_K_CHUNK_LEAF);
+            hipLaunchKernelGGL(k_chunk_bottom, dim3((unsigned)((total + BOT_BLOCK - 1) / BOT_BLOCK)),
+                               dim3(BOT_BLOCK), 0, st, plan->d_nodes, b0, b1 - b0, bb);
+            if (timer_end) timer_end(tctx, GSV_K_CHUNK_LEAF);
+        }
+        int g0 = p.lvl_gen_begin[h - 1], g1 = p.lvl_gen_end[h - 1];
+        if (g1 > g0) {
+            uint64_t total = (uint64_t)(g1 - g0) * nbodies;
+            if (timer_begin) timer_begin(tctx, GSV_K_CHUNK_LEVEL);
+            hipLaunchKernelGGL(k_chunk_level, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                               plan->d_nodes, plan->d_children, g0, g1 - g0, bb);
+            if (timer_end) timer_end(tctx, GSV_K_CHUNK_LEVEL);
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace gsv

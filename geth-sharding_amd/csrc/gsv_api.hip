@@ -1,0 +1,640 @@
+// C ABI of libgsv.so (include/gsv.h): context, device memory staging, launches, timing.
+// Host-pointer entry points stage through a grow-only device arena on the context's stream;
+// *_dev entry points take HBM-resident buffers and the caller's stream and never allocate or
+// synchronize (graph-capturable).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "chunk_root.h"
+#include "gsv_internal.h"
+#include "tx_host.h"
+
+struct gsv_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint4* gtab = nullptr;
+    // grow-only staging arena for the host-pointer entry points
+    uint8_t* arena = nullptr;
+    size_t arena_cap = 0;
+    std::mutex mu;
+    // kernel timing
+    int timing = 0;
+    struct Pending { int kid; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> free_events;
+    double total_ms[GSV_K_COUNT] = {0};
+    long launches[GSV_K_COUNT] = {0};
+    std::mutex tmu;
+    // chunk-root trie plans (per body length) and the device workspace of the *_dev paths
+    gsv::PlanCache plans;
+    uint8_t* work = nullptr;
+    size_t work_cap = 0;
+    std::vector<hipEvent_t> open_ev;  // timer events opened by launch hooks
+    hipStream_t cur_stream = nullptr;
+    std::mutex wmu;                   // serializes users of `work`
+};
+
+namespace {
+
+int hip_err(hipError_t e) { return e == hipSuccess ? GSV_SUCCESS : GSV_E_HIP; }
+
+#define HIPCHK(x)                                  \
+    do {                                           \
+        hipError_t _e = (x);                       \
+        if (_e != hipSuccess) return GSV_E_HIP;    \
+    } while (0)
+
+hipEvent_t take_event(gsv_ctx* c) {
+    if (!c->free_events.empty()) {
+        hipEvent_t e = c->free_events.back();
+        c->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+}
+
+// Brackets one launch with events on the launching stream when timing is on.
+struct KTimer {
+    gsv_ctx* c;
+    int kid;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    KTimer(gsv_ctx* c_, int kid_, hipStream_t st_) : c(c_), kid(kid_), st(st_) {
+        if (c->timing) {
+            std::lock_guard<std::mutex> g(c->tmu);
+            a = take_event(c);
+            b = take_event(c);
+            hipEventRecord(a, st);
+        }
+    }
+    ~KTimer() {
+        if (a) {
+            hipEventRecord(b, st);
+            std::lock_guard<std::mutex> g(c->tmu);
+            c->pending.push_back({kid, a, b});
+        }
+    }
+};
+
+void drain_timing(gsv_ctx* c) {
+    std::lock_guard<std::mutex> g(c->tmu);
+    for (auto& p : c->pending) {
+        hipEventSynchronize(p.b);
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->total_ms[p.kid] += ms;
+            c->launches[p.kid] += 1;
+        }
+        c->free_events.push_back(p.a);
+        c->free_events.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+// timer hooks for multi-launch paths (chunk root levels)
+void hook_begin(void* p, int kid) {
+    gsv_ctx* c = (gsv_ctx*)p;
+    if (!c->timing) return;
+    std::lock_guard<std::mutex> g(c->tmu);
+    hipEvent_t a = take_event(c);
+    hipEventRecord(a, c->cur_stream);
+    c->open_ev.push_back(a);
+}
+void hook_end(void* p, int kid) {
+    gsv_ctx* c = (gsv_ctx*)p;
+    if (!c->timing) return;
+    std::lock_guard<std::mutex> g(c->tmu);
+    hipEvent_t a = c->open_ev.back();
+    c->open_ev.pop_back();
+    hipEvent_t b = take_event(c);
+    hipEventRecord(b, c->cur_stream);
+    c->pending.push_back({kid, a, b});
+}
+
+int work_reserve(gsv_ctx* c, size_t bytes) {
+    if (bytes <= c->work_cap) return GSV_SUCCESS;
+    size_t cap = c->work_cap ? c->work_cap : (size_t)64 << 20;
+    while (cap < bytes) cap *= 2;
+    if (c->work) {
+        hipDeviceSynchronize();
+        hipFree(c->work);
+        c->work = nullptr;
+        c->work_cap = 0;
+    }
+    if (hipMalloc(&c->work, cap) != hipSuccess) return GSV_E_NOMEM;
+    c->work_cap = cap;
+    return GSV_SUCCESS;
+}
+
+int arena_reserve(gsv_ctx* c, size_t bytes) {
+    if (bytes <= c->arena_cap) return GSV_SUCCESS;
+    size_t cap = c->arena_cap ? c->arena_cap : (size_t)64 << 20;
+    while (cap < bytes) cap *= 2;
+    if (c->arena) {
+        hipStreamSynchronize(c->stream);
+        hipFree(c->arena);
+        c->arena = nullptr;
+        c->arena_cap = 0;
+    }
+    if (hipMalloc(&c->arena, cap) != hipSuccess) return GSV_E_NOMEM;
+    c->arena_cap = cap;
+    return GSV_SUCCESS;
+}
+
+// bump allocator over the arena (256-B aligned slices)
+struct Carve {
+    uint8_t* base;
+    size_t off = 0;
+    explicit Carve(uint8_t* b) : base(b) {}
+    template <typename T>
+    T* take(size_t bytes) {
+        T* p = (T*)(base + off);
+        off += (bytes + 255) & ~(size_t)255;
+        return p;
+    }
+};
+size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+int gsv_abi_version(void) { return GSV_ABI_VERSION; }
+
+int gsv_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* gsv_error_string(int err) {
+    switch (err) {
+        case GSV_SUCCESS: return "success";
+        case GSV_E_INVALID_ARG: return "invalid argument";
+        case GSV_E_HIP: return "HIP runtime error";
+        case GSV_E_NOMEM: return "out of device memory";
+        case GSV_E_NO_DEVICE: return "no HIP device";
+        case GSV_E_TOO_LARGE: return "input exceeds the reference size limit";
+        case GSV_E_RCCL: return "RCCL error";
+        default: return "unknown error";
+    }
+}
+
+int gsv_ctx_create(int device, gsv_ctx** out) {
+    if (!out) return GSV_E_INVALID_ARG;
+    *out = nullptr;
+    int n = gsv_device_count();
+    if (n <= 0) return GSV_E_NO_DEVICE;
+    if (device < 0 || device >= n) return GSV_E_INVALID_ARG;
+    HIPCHK(hipSetDevice(device));
+    gsv_ctx* c = new gsv_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return GSV_E_HIP;
+    }
+    if (hipMalloc(&c->gtab, gsv::GTAB_BYTES) != hipSuccess) {
+        hipStreamDestroy(c->stream);
+        delete c;
+        return GSV_E_NOMEM;
+    }
+    hipError_t e = gsv::launch_gtable_init(c->gtab, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        hipFree(c->gtab);
+        hipStreamDestroy(c->stream);
+        delete c;
+        return GSV_E_HIP;
+    }
+    *out = c;
+    return GSV_SUCCESS;
+}
+
+void gsv_ctx_destroy(gsv_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    drain_timing(c);
+    for (auto e : c->free_events) hipEventDestroy(e);
+    if (c->arena) hipFree(c->arena);
+    if (c->work) hipFree(c->work);
+    if (c->gtab) hipFree(c->gtab);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int gsv_ctx_set_timing(gsv_ctx* c, int enable) {
+    if (!c) return GSV_E_INVALID_ARG;
+    c->timing = enable ? 1 : 0;
+    return GSV_SUCCESS;
+}
+
+int gsv_ctx_kernel_time(gsv_ctx* c, int kid, double* total_ms, long* launches) {
+    if (!c || kid < 0 || kid >= GSV_K_COUNT) return GSV_E_INVALID_ARG;
+    drain_timing(c);
+    if (total_ms) *total_ms = c->total_ms[kid];
+    if (launches) *launches = c->launches[kid];
+    return GSV_SUCCESS;
+}
+
+int gsv_ctx_reset_timing(gsv_ctx* c) {
+    if (!c) return GSV_E_INVALID_ARG;
+    drain_timing(c);
+    for (int i = 0; i < GSV_K_COUNT; i++) {
+        c->total_ms[i] = 0;
+        c->launches[i] = 0;
+    }
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ Keccak-256
+int gsv_keccak256_batch_dev(gsv_ctx* c, const uint8_t* d_data, const uint64_t* d_off, size_t n,
+                            uint8_t* d_out32, void* stream) {
+    if (!c || (n && (!d_off || !d_out32)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    KTimer t(c, GSV_K_KECCAK, st);
+    return hip_err(gsv::launch_keccak256(d_data, d_off, (uint32_t)n, d_out32, st));
+}
+
+int gsv_keccak256_batch(gsv_ctx* c, const uint8_t* data, const uint64_t* off, size_t n,
+                        uint8_t* out32) {
+    if (!c || (n && (!off || !out32)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    size_t bytes = off[n] - off[0];
+    size_t need = al(bytes + 8) + al((n + 1) * 8) + al(n * 32);
+    int rc = arena_reserve(c, need);
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_data = cv.take<uint8_t>(bytes + 8);
+    uint64_t* d_off = cv.take<uint64_t>((n + 1) * 8);
+    uint8_t* d_out = cv.take<uint8_t>(n * 32);
+    std::vector<uint64_t> rel(n + 1);
+    for (size_t i = 0; i <= n; i++) rel[i] = off[i] - off[0];
+    if (bytes) HIPCHK(hipMemcpyAsync(d_data, data + off[0], bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_off, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    rc = gsv_keccak256_batch_dev(c, d_data, d_off, n, d_out, c->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out32, d_out, n * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ ecrecover
+int gsv_ecrecover_batch_dev(gsv_ctx* c, const uint8_t* d_msg32, const uint8_t* d_sig65, size_t n,
+                            uint8_t* d_pub65, uint8_t* d_addr20, uint8_t* d_status, void* stream) {
+    if (!c || (n && (!d_msg32 || !d_sig65 || !d_status)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    KTimer t(c, GSV_K_ECRECOVER, st);
+    return hip_err(gsv::launch_ecrecover(d_msg32, d_sig65, (uint32_t)n, c->gtab, d_pub65, d_addr20,
+                                         d_status, st));
+}
+
+int gsv_ecrecover_batch(gsv_ctx* c, const uint8_t* msg32, const uint8_t* sig65, size_t n,
+                        uint8_t* pub65_out, uint8_t* addr20_out, uint8_t* status) {
+    if (!c || (n && (!msg32 || !sig65 || !status)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    size_t need = al(n * 32) + al(n * 65) + al(n * 65) + al(n * 20) + al(n);
+    int rc = arena_reserve(c, need);
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_msg = cv.take<uint8_t>(n * 32);
+    uint8_t* d_sig = cv.take<uint8_t>(n * 65);
+    uint8_t* d_pub = cv.take<uint8_t>(n * 65);
+    uint8_t* d_addr = cv.take<uint8_t>(n * 20);
+    uint8_t* d_st = cv.take<uint8_t>(n);
+    HIPCHK(hipMemcpyAsync(d_msg, msg32, n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_sig, sig65, n * 65, hipMemcpyHostToDevice, c->stream));
+    rc = gsv_ecrecover_batch_dev(c, d_msg, d_sig, n, pub65_out ? d_pub : nullptr,
+                                 addr20_out ? d_addr : nullptr, d_st, c->stream);
+    if (rc) return rc;
+    if (pub65_out) HIPCHK(hipMemcpyAsync(pub65_out, d_pub, n * 65, hipMemcpyDeviceToHost, c->stream));
+    if (addr20_out) HIPCHK(hipMemcpyAsync(addr20_out, d_addr, n * 20, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ recoverPlain
+int gsv_sender_batch(gsv_ctx* c, const uint8_t* sighash32, const uint8_t* r32, const uint8_t* s32,
+                     const uint64_t* v, const uint8_t* v_big, size_t n, int homestead,
+                     uint8_t* addr20_out, uint8_t* status) {
+    if (!c || (n && (!sighash32 || !r32 || !s32 || !v || !v_big || !addr20_out || !status)) ||
+        n > 0xFFFFFFFFull)
+        return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    size_t need = 3 * al(n * 32) + al(n * 8) + al(n) + al(n * 20) + al(n);
+    int rc = arena_reserve(c, need);
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_h = cv.take<uint8_t>(n * 32);
+    uint8_t* d_r = cv.take<uint8_t>(n * 32);
+    uint8_t* d_s = cv.take<uint8_t>(n * 32);
+    uint64_t* d_v = cv.take<uint64_t>(n * 8);
+    uint8_t* d_vb = cv.take<uint8_t>(n);
+    uint8_t* d_a = cv.take<uint8_t>(n * 20);
+    uint8_t* d_st = cv.take<uint8_t>(n);
+    HIPCHK(hipMemcpyAsync(d_h, sighash32, n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_r, r32, n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_s, s32, n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_v, v, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_vb, v_big, n, hipMemcpyHostToDevice, c->stream));
+    {
+        KTimer t(c, GSV_K_ECRECOVER, c->stream);
+        HIPCHK(gsv::launch_sender(d_h, d_r, d_s, d_v, d_vb, (uint32_t)n, homestead, c->gtab, d_a, d_st,
+                                  c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(addr20_out, d_a, n * 20, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ synthetic signer (bench data)
+int gsv_synth_sign_dev(gsv_ctx* c, uint64_t seed, size_t n, uint8_t* d_msg32, uint8_t* d_sig65,
+                       uint8_t* d_pub65, uint8_t* d_addr20, void* stream) {
+    if (!c || (n && (!d_msg32 || !d_sig65)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return hip_err(gsv::launch_synth_sign(seed, (uint32_t)n, c->gtab, d_msg32, d_sig65, d_pub65,
+                                          d_addr20, st));
+}
+
+int gsv_synth_sign(gsv_ctx* c, uint64_t seed, size_t n, uint8_t* msg32, uint8_t* sig65,
+                   uint8_t* pub65, uint8_t* addr20) {
+    if (!c || (n && (!msg32 || !sig65)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    size_t need = al(n * 32) + 2 * al(n * 65) + al(n * 20);
+    int rc = arena_reserve(c, need);
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_m = cv.take<uint8_t>(n * 32);
+    uint8_t* d_s = cv.take<uint8_t>(n * 65);
+    uint8_t* d_p = cv.take<uint8_t>(n * 65);
+    uint8_t* d_a = cv.take<uint8_t>(n * 20);
+    rc = gsv_synth_sign_dev(c, seed, n, d_m, d_s, pub65 ? d_p : nullptr, addr20 ? d_a : nullptr,
+                            c->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(msg32, d_m, n * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(sig65, d_s, n * 65, hipMemcpyDeviceToHost, c->stream));
+    if (pub65) HIPCHK(hipMemcpyAsync(pub65, d_p, n * 65, hipMemcpyDeviceToHost, c->stream));
+    if (addr20) HIPCHK(hipMemcpyAsync(addr20, d_a, n * 20, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ chunk root
+static const uint8_t EMPTY_ROOT[32] = {0x56, 0xe8, 0x1f, 0x17, 0x1b, 0xcc, 0x55, 0xa6, 0xff, 0x83, 0x45,
+                                       0xe6, 0x92, 0xc0, 0xf8, 0x6e, 0x5b, 0x48, 0xe0, 0x1b, 0x99, 0x6c,
+                                       0xad, 0xc0, 0x01, 0x62, 0x2f, 0xb5, 0xe3, 0x63, 0xb4, 0x21};
+static const uint64_t MAX_BODY = 1ull << 20;  // collationSizelimit (sharding/collation.go:45)
+
+// Body i = d_bodies[start[i] .. end[i]); roots to d_roots (device) via workspace `work`.
+static int chunk_root_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* start,
+                               const uint64_t* end, size_t n, uint8_t* d_roots, hipStream_t st) {
+    // group bodies by length (the trie shape depends only on N)
+    std::map<uint64_t, std::vector<uint32_t>> groups;
+    for (size_t i = 0; i < n; i++) {
+        if (end[i] < start[i] || end[i] - start[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+        groups[end[i] - start[i]].push_back((uint32_t)i);
+    }
+    size_t need = 0;
+    for (auto& g : groups) {
+        if (g.first == 0) continue;
+        gsv::TriePlan* pl = c->plans.get((uint32_t)g.first);
+        if (!pl) return GSV_E_NOMEM;
+        need += al(g.second.size() * 8) + al(g.second.size() * 32) +
+                al(gsv::chunk_root_scratch_bytes(pl, (uint32_t)g.second.size()));
+    }
+    int rc = work_reserve(c, need + 4096);
+    if (rc) return rc;
+    Carve cv(c->work);
+    c->cur_stream = st;
+    std::vector<std::vector<uint64_t>> host_offs;
+    host_offs.reserve(groups.size());
+    for (auto& g : groups) {
+        const auto& idx = g.second;
+        if (g.first == 0) {  // empty trie -> emptyRoot (trie/trie.go:472-474)
+            for (uint32_t i : idx)
+                HIPCHK(hipMemcpyAsync(d_roots + (size_t)i * 32, EMPTY_ROOT, 32, hipMemcpyHostToDevice, st));
+            continue;
+        }
+        gsv::TriePlan* pl = c->plans.get((uint32_t)g.first);
+        uint64_t* d_off = cv.take<uint64_t>(idx.size() * 8);
+        uint8_t* d_gr = cv.take<uint8_t>(idx.size() * 32);
+        uint8_t* d_scr = cv.take<uint8_t>(gsv::chunk_root_scratch_bytes(pl, (uint32_t)idx.size()));
+        host_offs.emplace_back(idx.size());
+        auto& ho = host_offs.back();
+        for (size_t k = 0; k < idx.size(); k++) ho[k] = start[idx[k]];
+        HIPCHK(hipMemcpyAsync(d_off, ho.data(), ho.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(gsv::launch_chunk_root_plan(pl, d_bodies, d_off, (uint32_t)idx.size(), d_scr, d_gr, st,
+                                           hook_begin, hook_end, c));
+        // scatter group roots to their positions (contiguous runs copied together)
+        size_t k = 0;
+        while (k < idx.size()) {
+            size_t e2 = k + 1;
+            while (e2 < idx.size() && idx[e2] == idx[e2 - 1] + 1) e2++;
+            HIPCHK(hipMemcpyAsync(d_roots + (size_t)idx[k] * 32, d_gr + k * 32, (e2 - k) * 32,
+                                  hipMemcpyDeviceToDevice, st));
+            k = e2;
+        }
+    }
+    HIPCHK(hipStreamSynchronize(st));  // host offset staging must outlive the async copies
+    return GSV_SUCCESS;
+}
+
+int gsv_chunk_root_batch_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n,
+                             uint8_t* d_root32_out, void* stream) {
+    if (!c || (n && (!h_off || !d_root32_out || !d_bodies))) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->wmu);
+    HIPCHK(hipSetDevice(c->device));
+    return chunk_root_dev_impl(c, d_bodies, h_off, h_off + 1, n, d_root32_out,
+                               stream ? (hipStream_t)stream : c->stream);
+}
+
+int gsv_chunk_root_batch(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n, uint8_t* root32_out) {
+    if (!c || (n && (!off || !root32_out))) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    for (size_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    // stage bodies in HBM with 16-byte aligned starts (vector loads in the bottom-level kernel)
+    std::vector<uint64_t> st(n), en(n);
+    uint64_t pos = 0;
+    for (size_t i = 0; i < n; i++) {
+        st[i] = pos;
+        en[i] = pos + (off[i + 1] - off[i]);
+        pos = (en[i] + 15) & ~15ull;
+    }
+    int rc = arena_reserve(c, al(pos + 16) + al(n * 32));
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_b = cv.take<uint8_t>(pos + 16);
+    uint8_t* d_r = cv.take<uint8_t>(n * 32);
+    for (size_t i = 0; i < n; i++)
+        if (en[i] > st[i])
+            HIPCHK(hipMemcpyAsync(d_b + st[i], bodies + off[i], en[i] - st[i], hipMemcpyHostToDevice, c->stream));
+    {
+        std::lock_guard<std::mutex> g2(c->wmu);
+        rc = chunk_root_dev_impl(c, d_b, st.data(), en.data(), n, d_r, c->stream);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(root32_out, d_r, n * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ types.Sender over tx RLP
+// Host: decode + sighash preimages (threads). GPU: Keccak of the preimages, recoverPlain + address.
+static int tx_sender_impl(gsv_ctx* c, const uint8_t* rlp, const uint64_t* off, size_t n, const uint8_t* cid,
+                          size_t cidlen, int signer_kind, uint8_t* addr_out, uint8_t* status_out) {
+    std::vector<uint8_t> hst(n), rr(n * 32), ss(n * 32), vb(n);
+    std::vector<uint64_t> vv(n), plen(n);
+    std::vector<std::vector<uint8_t>> pres;
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < 4096) nt = 1;
+    std::vector<std::vector<uint8_t>> tpre(nt);
+    std::vector<std::thread> th;
+    auto work = [&](unsigned t) {
+        size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+        gsv::TxPrep p;
+        for (size_t i = lo; i < hi; i++) {
+            int st = gsv::tx_prepare(rlp + off[i], off[i + 1] - off[i], cid, cidlen, signer_kind, p);
+            hst[i] = (uint8_t)st;
+            if (st != GSV_ST_OK) {
+                plen[i] = 0;
+                vb[i] = 1;
+                continue;
+            }
+            memcpy(&rr[i * 32], p.r32, 32);
+            memcpy(&ss[i * 32], p.s32, 32);
+            vv[i] = p.v;
+            vb[i] = p.vbig;
+            plen[i] = p.pre.size();
+            tpre[t].insert(tpre[t].end(), p.pre.begin(), p.pre.end());
+        }
+    };
+    for (unsigned t = 0; t < nt; t++) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+    std::vector<uint64_t> poff(n + 1);
+    poff[0] = 0;
+    for (size_t i = 0; i < n; i++) poff[i + 1] = poff[i] + plen[i];
+    size_t pbytes = poff[n];
+    int homestead = signer_kind == GSV_SIGNER_FRONTIER ? 0 : 1;
+    size_t need = al(pbytes + 8) + al((n + 1) * 8) + 3 * al(n * 32) + al(n * 8) + al(n) + al(n * 20) + al(n);
+    int rc = arena_reserve(c, need);
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_pre = cv.take<uint8_t>(pbytes + 8);
+    uint64_t* d_poff = cv.take<uint64_t>((n + 1) * 8);
+    uint8_t* d_h = cv.take<uint8_t>(n * 32);
+    uint8_t* d_r = cv.take<uint8_t>(n * 32);
+    uint8_t* d_s = cv.take<uint8_t>(n * 32);
+    uint64_t* d_v = cv.take<uint64_t>(n * 8);
+    uint8_t* d_vb = cv.take<uint8_t>(n);
+    uint8_t* d_a = cv.take<uint8_t>(n * 20);
+    uint8_t* d_st = cv.take<uint8_t>(n);
+    size_t w = 0;
+    for (unsigned t = 0; t < nt; t++) {
+        if (!tpre[t].empty())
+            HIPCHK(hipMemcpyAsync(d_pre + w, tpre[t].data(), tpre[t].size(), hipMemcpyHostToDevice, c->stream));
+        w += tpre[t].size();
+    }
+    HIPCHK(hipMemcpyAsync(d_poff, poff.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_r, rr.data(), n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_s, ss.data(), n * 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_v, vv.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_vb, vb.data(), n, hipMemcpyHostToDevice, c->stream));
+    {
+        KTimer t(c, GSV_K_SENDER_PREP, c->stream);
+        HIPCHK(gsv::launch_keccak256(d_pre, d_poff, (uint32_t)n, d_h, c->stream));
+    }
+    {
+        KTimer t(c, GSV_K_ECRECOVER, c->stream);
+        HIPCHK(gsv::launch_sender(d_h, d_r, d_s, d_v, d_vb, (uint32_t)n, homestead, c->gtab, d_a, d_st, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(addr_out, d_a, n * 20, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(status_out, d_st, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < n; i++)
+        if (hst[i] != GSV_ST_OK) {
+            status_out[i] = hst[i];
+            memset(addr_out + i * 20, 0, 20);
+        }
+    return GSV_SUCCESS;
+}
+
+int gsv_tx_sender_batch(gsv_ctx* c, const uint8_t* rlp, const uint64_t* off, size_t n, const uint8_t* chain_id,
+                        size_t chain_id_len, int signer_kind, uint8_t* addr20_out, uint8_t* status) {
+    if (!c || (n && (!rlp || !off || !addr20_out || !status)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    if (signer_kind < GSV_SIGNER_EIP155 || signer_kind > GSV_SIGNER_FRONTIER) return GSV_E_INVALID_ARG;
+    if (chain_id_len && !chain_id) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    return tx_sender_impl(c, rlp, off, n, chain_id, chain_id_len, signer_kind, addr20_out, status);
+}
+
+// ------------------------------------------------------------------ notary validation (Cfg4)
+int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n_shards,
+                               const uint8_t* chain_id, size_t chain_id_len, uint32_t max_txs,
+                               uint8_t* root32_out, uint32_t* ntx_out, uint8_t* valid_bitmap_out,
+                               uint8_t* senders_out) {
+    if (!c || (n_shards && (!bodies || !off || !root32_out || !ntx_out || !valid_bitmap_out))) return GSV_E_INVALID_ARG;
+    if (chain_id_len && !chain_id) return GSV_E_INVALID_ARG;
+    if (n_shards == 0) return GSV_SUCCESS;
+    // 1. chunk roots (GPU)
+    int rc = gsv_chunk_root_batch(c, bodies, off, n_shards, root32_out);
+    if (rc) return rc;
+    // 2. blob-deserialize each body into tx RLPs (sharding/collation.go:193-206)
+    std::vector<uint8_t> txdata;
+    std::vector<uint64_t> boff;
+    std::vector<size_t> first(n_shards + 1);
+    for (size_t s = 0; s < n_shards; s++) {
+        first[s] = boff.size() / 2;
+        gsv::blob_deserialize(bodies + off[s], off[s + 1] - off[s], txdata, boff);
+    }
+    first[n_shards] = boff.size() / 2;
+    size_t ntx = first[n_shards];
+    std::vector<uint64_t> toff(ntx + 1, 0);
+    for (size_t t = 0; t < ntx; t++) toff[t] = boff[2 * t];
+    if (ntx) toff[ntx] = boff[2 * ntx - 1];
+    // blobs are contiguous in txdata (each blob's end == next blob's start)
+    std::vector<uint8_t> addr(ntx * 20), st(ntx);
+    if (ntx) {
+        std::lock_guard<std::mutex> g(c->mu);
+        HIPCHK(hipSetDevice(c->device));
+        txdata.push_back(0);
+        rc = tx_sender_impl(c, txdata.data(), toff.data(), ntx, chain_id, chain_id_len, GSV_SIGNER_EIP155,
+                            addr.data(), st.data());
+        if (rc) return rc;
+    }
+    size_t bm_bytes = (max_txs + 7) / 8;
+    memset(valid_bitmap_out, 0, bm_bytes * n_shards);
+    for (size_t s = 0; s < n_shards; s++) {
+        size_t cnt = first[s + 1] - first[s];
+        ntx_out[s] = (uint32_t)cnt;
+        for (size_t t = 0; t < cnt && t < max_txs; t++)
+            if (st[first[s] + t] == GSV_ST_OK) valid_bitmap_out[s * bm_bytes + t / 8] |= (uint8_t)(1u << (t % 8));
+    }
+    if (senders_out && ntx) memcpy(senders_out, addr.data(), ntx * 20);
+    return GSV_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,35 @@
+// Internal declarations shared by the HIP translation units of libgsv.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gsv.h"
+
+namespace gsv {
+
+// ecrecover.hip
+hipError_t launch_gtable_init(uint4* gtab, hipStream_t st);
+hipError_t launch_ecrecover(const uint8_t* msg32, const uint8_t* sig65, uint32_t n, const uint4* gtab,
+                            uint8_t* pub65, uint8_t* addr20, uint8_t* status, hipStream_t st);
+hipError_t launch_sender(const uint8_t* sighash32, const uint8_t* r32, const uint8_t* s32,
+                         const uint64_t* v, const uint8_t* vbig, uint32_t n, int homestead,
+                         const uint4* gtab, uint8_t* addr20, uint8_t* status, hipStream_t st);
+hipError_t launch_synth_sign(uint64_t seed, uint32_t n, const uint4* gtab, uint8_t* msg32,
+                             uint8_t* sig65, uint8_t* pub65, uint8_t* addr20, hipStream_t st);
+
+// keccak.hip
+hipError_t launch_keccak256(const uint8_t* data, const uint64_t* off, uint32_t n, uint8_t* out32,
+                            hipStream_t st);
+
+// chunk_root.hip
+struct TriePlan;  // host-built, device-resident trie shape for one body length N
+size_t chunk_root_scratch_bytes(const TriePlan* plan, uint32_t nbodies);
+hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies, const uint64_t* d_body_off,
+                                  uint32_t nbodies, uint8_t* d_scratch, uint8_t* d_roots, hipStream_t st,
+                                  void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
+                                  void* tctx);
+
+constexpr size_t GTAB_ENTRIES = 32 * 256;
+constexpr size_t GTAB_BYTES = GTAB_ENTRIES * 64;
+
+}  // namespace gsv

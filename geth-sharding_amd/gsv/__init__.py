@@ -1,0 +1,223 @@
+"""gsv — MI355X-native batch validation engine for geth-sharding's collation-validation hot path.
+
+Host-side mirror of the reference's Go APIs for this path, over the C ABI of libgsv.so
+(include/gsv.h).  Every call runs the hand-written HIP kernels for gfx950; there is no CPU
+fallback (a missing libgsv.so or GPU raises).
+
+    crypto.Ecrecover / SigToPub / Keccak256      crypto/signature_cgo.go:31-44, crypto/crypto.go:43
+    types.Sender + EIP155/Homestead/Frontier     core/types/transaction_signing.go:72-247
+    sharding.CalculateChunkRoot / DeriveSha      sharding/collation.go:115-119, core/types/derive_sha.go:32
+    bn256.PairingCheck / precompile Run          crypto/bn256/cloudflare/bn256.go:313-327, core/vm/contracts.go:333
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from . import _lib
+from ._lib import GsvError, check
+
+__all__ = ["Context", "default_context", "GsvError", "device_count"]
+
+
+def _np_u8(a) -> np.ndarray:
+    if isinstance(a, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(a), np.uint8)
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def _ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+def _pack(msgs):
+    """list of bytes -> (flat uint8 array, uint64 offsets[n+1])"""
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=len(msgs))
+    off = np.zeros(len(msgs) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    flat = np.frombuffer(b"".join(bytes(m) for m in msgs) + b"\0" * 8, np.uint8)
+    return flat, off
+
+
+def device_count() -> int:
+    return int(_lib.load().gsv_device_count())
+
+
+class Context:
+    """One libgsv context (one HIP device): stream, HBM staging arena, precomputed tables."""
+
+    def __init__(self, device: int = 0):
+        L = _lib.load()
+        h = ctypes.c_void_p()
+        check(L.gsv_ctx_create(int(device), ctypes.byref(h)))
+        self._h = h
+        self.device = int(device)
+
+    # -------------------------------------------------------------- lifecycle / timing
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().gsv_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_timing(self, on: bool):
+        check(_lib.load().gsv_ctx_set_timing(self._h, 1 if on else 0))
+
+    def kernel_time(self, kid: int):
+        ms = ctypes.c_double()
+        n = ctypes.c_long()
+        check(_lib.load().gsv_ctx_kernel_time(self._h, kid, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def reset_timing(self):
+        check(_lib.load().gsv_ctx_reset_timing(self._h))
+
+    # -------------------------------------------------------------- Keccak-256
+    def keccak256_batch(self, msgs) -> np.ndarray:
+        n = len(msgs)
+        out = np.zeros((n, 32), np.uint8)
+        if n == 0:
+            return out
+        flat, off = _pack(msgs)
+        check(_lib.load().gsv_keccak256_batch(self._h, _ptr(flat), _ptr(off), n, _ptr(out)))
+        return out
+
+    # -------------------------------------------------------------- secp256k1
+    def ecrecover_batch(self, msg32, sig65, want_pub=True, want_addr=False):
+        """msg32 (n,32) uint8, sig65 (n,65) uint8 -> (pub65 (n,65) | None, addr20 (n,20) | None,
+        status (n,))  with ext.h / secp256.go semantics per item."""
+        msg32 = np.ascontiguousarray(msg32, np.uint8).reshape(-1, 32)
+        sig65 = np.ascontiguousarray(sig65, np.uint8).reshape(-1, 65)
+        n = msg32.shape[0]
+        if sig65.shape[0] != n:
+            raise ValueError("msg32 and sig65 batch sizes differ")
+        pub = np.zeros((n, 65), np.uint8) if want_pub else None
+        addr = np.zeros((n, 20), np.uint8) if want_addr else None
+        st = np.zeros(n, np.uint8)
+        if n:
+            check(_lib.load().gsv_ecrecover_batch(self._h, _ptr(msg32), _ptr(sig65), n, _ptr(pub),
+                                                  _ptr(addr), _ptr(st)))
+        return pub, addr, st
+
+    def sender_batch(self, sighash32, r32, s32, v, v_big, homestead: bool):
+        sighash32 = np.ascontiguousarray(sighash32, np.uint8).reshape(-1, 32)
+        n = sighash32.shape[0]
+        r32 = np.ascontiguousarray(r32, np.uint8).reshape(n, 32)
+        s32 = np.ascontiguousarray(s32, np.uint8).reshape(n, 32)
+        v = np.ascontiguousarray(v, np.uint64).reshape(n)
+        v_big = np.ascontiguousarray(v_big, np.uint8).reshape(n)
+        addr = np.zeros((n, 20), np.uint8)
+        st = np.zeros(n, np.uint8)
+        if n:
+            check(_lib.load().gsv_sender_batch(self._h, _ptr(sighash32), _ptr(r32), _ptr(s32), _ptr(v),
+                                               _ptr(v_big), n, 1 if homestead else 0, _ptr(addr),
+                                               _ptr(st)))
+        return addr, st
+
+    def tx_sender_batch(self, txs, chain_id: int, signer_kind: int):
+        n = len(txs)
+        addr = np.zeros((n, 20), np.uint8)
+        st = np.zeros(n, np.uint8)
+        if n == 0:
+            return addr, st
+        flat, off = _pack(txs)
+        cid = np.frombuffer(_be(chain_id) + b"\0", np.uint8)
+        check(_lib.load().gsv_tx_sender_batch(self._h, _ptr(flat), _ptr(off), n, _ptr(cid),
+                                              len(_be(chain_id)), int(signer_kind), _ptr(addr),
+                                              _ptr(st)))
+        return addr, st
+
+    def synth_sign(self, seed: int, n: int, want_pub=True, want_addr=True):
+        msg = np.zeros((n, 32), np.uint8)
+        sig = np.zeros((n, 65), np.uint8)
+        pub = np.zeros((n, 65), np.uint8) if want_pub else None
+        addr = np.zeros((n, 20), np.uint8) if want_addr else None
+        if n:
+            check(_lib.load().gsv_synth_sign(self._h, ctypes.c_uint64(seed), n, _ptr(msg), _ptr(sig),
+                                             _ptr(pub), _ptr(addr)))
+        return msg, sig, pub, addr
+
+    # -------------------------------------------------------------- device-resident (torch) paths
+    def ecrecover_batch_dev(self, msg_t, sig_t, pub_t, addr_t, st_t, stream=None):
+        """torch uint8 CUDA tensors already in HBM; enqueues on `stream` (torch stream or None)."""
+        n = msg_t.shape[0]
+        sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        check(_lib.load().gsv_ecrecover_batch_dev(
+            self._h, ctypes.c_void_p(msg_t.data_ptr()), ctypes.c_void_p(sig_t.data_ptr()), n,
+            ctypes.c_void_p(pub_t.data_ptr()) if pub_t is not None else None,
+            ctypes.c_void_p(addr_t.data_ptr()) if addr_t is not None else None,
+            ctypes.c_void_p(st_t.data_ptr()), sp))
+
+    def synth_sign_dev(self, seed, msg_t, sig_t, pub_t=None, addr_t=None, stream=None):
+        n = msg_t.shape[0]
+        sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        check(_lib.load().gsv_synth_sign_dev(
+            self._h, ctypes.c_uint64(seed), n, ctypes.c_void_p(msg_t.data_ptr()),
+            ctypes.c_void_p(sig_t.data_ptr()),
+            ctypes.c_void_p(pub_t.data_ptr()) if pub_t is not None else None,
+            ctypes.c_void_p(addr_t.data_ptr()) if addr_t is not None else None, sp))
+
+    def keccak256_batch_dev(self, data_t, off_t, out_t, stream=None):
+        n = out_t.shape[0]
+        sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        check(_lib.load().gsv_keccak256_batch_dev(self._h, ctypes.c_void_p(data_t.data_ptr()),
+                                                  ctypes.c_void_p(off_t.data_ptr()), n,
+                                                  ctypes.c_void_p(out_t.data_ptr()), sp))
+
+
+def _be(x: int) -> bytes:
+    return x.to_bytes((x.bit_length() + 7) // 8, "big") if x else b""
+
+
+_default = None
+_default_lock = threading.Lock()
+
+
+def default_context() -> Context:
+    """Process-wide context on LOCAL_RANK's device (one process per GPU), created on first use,
+    like the reference's global secp256k1 context (crypto/secp256k1/secp256.go:45-52)."""
+    global _default
+    with _default_lock:
+        if _default is None:
+            dev = int(os.environ.get("LOCAL_RANK", "0"))
+            n = device_count()
+            if n <= 0:
+                raise GsvError("no HIP device visible: libgsv requires an MI355X (gfx950)")
+            _default = Context(dev % n)
+    return _default
+
+
+def _chunk_root_batch(self, bodies) -> np.ndarray:
+    """DeriveSha(Chunks(body)) for each body (sharding/collation.go:115-119)."""
+    n = len(bodies)
+    out = np.zeros((n, 32), np.uint8)
+    if n == 0:
+        return out
+    flat, off = _pack(bodies)
+    check(_lib.load().gsv_chunk_root_batch(self._h, _ptr(flat), _ptr(off), n, _ptr(out)))
+    return out
+
+
+def _chunk_root_batch_dev(self, bodies_t, h_off, roots_t, stream=None):
+    """bodies_t: torch uint8 CUDA tensor holding all bodies; h_off: numpy uint64 offsets (n+1)."""
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    n = h_off.shape[0] - 1
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_chunk_root_batch_dev(self._h, ctypes.c_void_p(bodies_t.data_ptr()), _ptr(h_off), n,
+                                               ctypes.c_void_p(roots_t.data_ptr()), sp))
+
+
+Context.chunk_root_batch = _chunk_root_batch
+Context.chunk_root_batch_dev = _chunk_root_batch_dev

@@ -1,0 +1,172 @@
+/*
+ * gsv.h — C ABI of the MI355X-native batch validation engine for geth-sharding's
+ * collation-validation hot path (libgsv.so, HIP for gfx950).
+ *
+ * Plain C linkage, plain pointers and sizes, no torch / HIP types in the signatures, so
+ * the reference's Go side can bind it with a cgo preamble exactly as it binds
+ * crypto/secp256k1/ext.h today (see INTEGRATION.md for the stub).
+ *
+ * Every entry point replaces a per-item reference call with a batch:
+ *   gsv_ecrecover_batch        <- secp256k1_ext_ecdsa_recover (crypto/secp256k1/ext.h:30-47)
+ *                                 via secp256k1.RecoverPubkey (crypto/secp256k1/secp256.go:105-122)
+ *                                 / crypto.Ecrecover (crypto/signature_cgo.go:31)
+ *   gsv_sender_batch           <- recoverPlain (core/types/transaction_signing.go:222-247)
+ *                                 + crypto.ValidateSignatureValues (crypto/crypto.go:181-192)
+ *   gsv_tx_sender_batch        <- types.Sender(signer, tx) (core/types/transaction_signing.go:72-89,
+ *                                 127-137, 182-184, 218-220) over RLP-encoded txs
+ *   gsv_keccak256_batch        <- crypto.Keccak256 (crypto/crypto.go:43-49; crypto/sha3/hashes.go:16)
+ *   gsv_chunk_root_batch       <- Collation.CalculateChunkRoot (sharding/collation.go:115-119)
+ *                                 = types.DeriveSha(Chunks(body)) (core/types/derive_sha.go:32-41)
+ *   gsv_bn256_pairing_check_batch <- bn256.PairingCheck (crypto/bn256/cloudflare/bn256.go:313-327)
+ *                                 as driven by the bn256Pairing precompile (core/vm/contracts.go:333-360)
+ *   gsv_notary_validate_shards <- the notary's per-collation validation (sharding/notary/notary.go:413-496
+ *                                 + sharding/collation.go:193-206 DeserializeBlobToTx + Sender)
+ *
+ * Conventions
+ *   - Return value: GSV_SUCCESS (0) or a negative GSV_E_* API/HIP error. A bad ITEM never fails
+ *     the batch: it gets a per-item status code (GSV_ST_*) mirroring the reference's errors.
+ *   - Host-pointer entry points copy inputs to HBM, run, and copy results back (synchronous).
+ *   - *_dev entry points take DEVICE pointers already resident in HBM and a hipStream_t passed
+ *     as void*; they enqueue and return (asynchronous, graph-capturable: no allocation or sync).
+ *   - One gsv_ctx per device; a context is safe to use from several threads on distinct streams
+ *     for the *_dev calls; host-pointer calls serialize on the context's internal stream.
+ */
+#ifndef GSV_H
+#define GSV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSV_ABI_VERSION 1
+
+/* ---- API / HIP errors (return values) ---- */
+#define GSV_SUCCESS 0
+#define GSV_E_INVALID_ARG (-1)
+#define GSV_E_HIP (-2)
+#define GSV_E_NOMEM (-3)
+#define GSV_E_NO_DEVICE (-4)
+#define GSV_E_TOO_LARGE (-5) /* e.g. collation body > 2^20 (sharding/collation.go:45) */
+#define GSV_E_RCCL (-6)
+
+/* ---- per-item status codes (mirror the reference's error values) ---- */
+#define GSV_ST_OK 0
+#define GSV_ST_INVALID_MSG_LEN 1   /* secp256k1.ErrInvalidMsgLen       secp256.go:55 */
+#define GSV_ST_INVALID_SIG_LEN 2   /* secp256k1.ErrInvalidSignatureLen secp256.go:56 */
+#define GSV_ST_INVALID_RECID 3     /* secp256k1.ErrInvalidRecoveryID   secp256.go:57 */
+#define GSV_ST_RECOVER_FAILED 4    /* secp256k1.ErrRecoverFailed       secp256.go:61 */
+#define GSV_ST_INVALID_SIG 5       /* types.ErrInvalidSig              transaction.go:35 */
+#define GSV_ST_INVALID_CHAIN_ID 6  /* types.ErrInvalidChainId          transaction_signing.go */
+#define GSV_ST_INVALID_PUBKEY 7    /* "invalid public key"             transaction_signing.go:240 */
+#define GSV_ST_BAD_RLP 8           /* rlp decode error of the tx */
+#define GSV_ST_BN_BAD_INPUT 9      /* bn256 unmarshal / curve / subgroup failure */
+
+/* signer kinds for gsv_tx_sender_batch (core/types/transaction_signing.go) */
+#define GSV_SIGNER_EIP155 0
+#define GSV_SIGNER_HOMESTEAD 1
+#define GSV_SIGNER_FRONTIER 2
+
+/* pairing verdicts (core/vm/contracts.go:333-360: true32 / false32 / errBadPairingInput) */
+#define GSV_PAIRING_FALSE 0
+#define GSV_PAIRING_TRUE 1
+#define GSV_PAIRING_BAD_INPUT 2
+
+typedef struct gsv_ctx gsv_ctx;
+
+/* ---- context ---- */
+int gsv_device_count(void);
+/* Creates a context on HIP device `device`; builds the device-resident precomputed tables
+ * (secp256k1 fixed-base comb, Keccak round constants). ~once per process, like the reference's
+ * global secp256k1 context (crypto/secp256k1/secp256.go:45-52). */
+int gsv_ctx_create(int device, gsv_ctx **out);
+void gsv_ctx_destroy(gsv_ctx *ctx);
+const char *gsv_error_string(int err);
+int gsv_abi_version(void);
+
+/* Kernel timing (HIP events around each launch on the launching stream; off by default). */
+int gsv_ctx_set_timing(gsv_ctx *ctx, int enable);
+/* kernel ids for gsv_ctx_kernel_time */
+#define GSV_K_KECCAK 0
+#define GSV_K_ECRECOVER 1
+#define GSV_K_CHUNK_LEAF 2
+#define GSV_K_CHUNK_LEVEL 3
+#define GSV_K_PAIRING 4
+#define GSV_K_SENDER_PREP 5
+#define GSV_K_COUNT 8
+/* total milliseconds and launch count accumulated for kernel `kid` since the last reset */
+int gsv_ctx_kernel_time(gsv_ctx *ctx, int kid, double *total_ms, long *launches);
+int gsv_ctx_reset_timing(gsv_ctx *ctx);
+
+/* ---- Keccak-256 (A10) ----
+ * Message i is data[off[i] .. off[i+1]); out32[32*i .. +32) = Keccak256(message i). */
+int gsv_keccak256_batch(gsv_ctx *ctx, const uint8_t *data, const uint64_t *off, size_t n,
+                        uint8_t *out32);
+int gsv_keccak256_batch_dev(gsv_ctx *ctx, const uint8_t *d_data, const uint64_t *d_off, size_t n,
+                            uint8_t *d_out32, void *stream);
+
+/* ---- secp256k1 public-key recovery (A5-A9) ----
+ * msg32: n x 32 B message hashes; sig65: n x 65 B [R || S || recid].
+ * pub65_out: n x 65 B uncompressed keys (0x04 || X || Y), zeroed for failed items.
+ * status: GSV_ST_OK / GSV_ST_INVALID_RECID (recid >= 4) / GSV_ST_RECOVER_FAILED.
+ * addr20_out (optional, may be NULL): Keccak256(X || Y)[12:32] for OK items. */
+int gsv_ecrecover_batch(gsv_ctx *ctx, const uint8_t *msg32, const uint8_t *sig65, size_t n,
+                        uint8_t *pub65_out, uint8_t *addr20_out, uint8_t *status);
+int gsv_ecrecover_batch_dev(gsv_ctx *ctx, const uint8_t *d_msg32, const uint8_t *d_sig65, size_t n,
+                            uint8_t *d_pub65_out, uint8_t *d_addr20_out, uint8_t *d_status,
+                            void *stream);
+
+/* ---- recoverPlain (A4): sighash + (R, S, V) -> sender address ----
+ * r32/s32: n x 32 B big-endian; v: per-item V already reduced by the signer
+ * (27/28 for Homestead/Frontier, tx.V - 2*chainId - 8 for EIP-155) as a uint64 with
+ * v_big[i] != 0 meaning "V had more than 8 bits" (-> GSV_ST_INVALID_SIG).
+ * homestead: 1 = reject s > n/2 (crypto/crypto.go:188). */
+int gsv_sender_batch(gsv_ctx *ctx, const uint8_t *sighash32, const uint8_t *r32, const uint8_t *s32,
+                     const uint64_t *v, const uint8_t *v_big, size_t n, int homestead,
+                     uint8_t *addr20_out, uint8_t *status);
+
+/* ---- types.Sender over RLP-encoded transactions (A1-A4) ----
+ * tx i = rlp[off[i] .. off[i+1]); chain_id big-endian (len 0 = 0). */
+int gsv_tx_sender_batch(gsv_ctx *ctx, const uint8_t *rlp, const uint64_t *off, size_t n,
+                        const uint8_t *chain_id, size_t chain_id_len, int signer_kind,
+                        uint8_t *addr20_out, uint8_t *status);
+
+/* ---- collation chunk root (B1-B5) ----
+ * body i = bodies[off[i] .. off[i+1]), each <= 2^20 bytes (else GSV_E_TOO_LARGE).
+ * root32_out[i] = DeriveSha(Chunks(body i)); an empty body gives emptyRoot. */
+int gsv_chunk_root_batch(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off, size_t n,
+                         uint8_t *root32_out);
+int gsv_chunk_root_batch_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off, size_t n,
+                             uint8_t *d_root32_out, void *stream);
+
+/* ---- BN254 pairing check (C1-C6) ----
+ * check i = in[off[i] .. off[i+1]) in the precompile encoding (k x 192 B);
+ * verdict[i] = GSV_PAIRING_TRUE / FALSE / BAD_INPUT. */
+int gsv_bn256_pairing_check_batch(gsv_ctx *ctx, const uint8_t *in, const uint64_t *off, size_t n,
+                                  uint8_t *verdict);
+
+/* ---- synthetic signed workload (bench / test data generator; signing is not on the path) ----
+ * key_i, msg_i, nonce_i = Keccak256(le64(seed) || le64(i) || "key"/"msg"/"nce"), key and nonce
+ * reduced mod n (0 -> 1); sig_i = ECDSA(key_i, msg_i, nonce_i), low-s normalised, recid in sig[64].
+ * pub65/addr20 (optional) receive the signer's key and address (the expected recovery result). */
+int gsv_synth_sign(gsv_ctx *ctx, uint64_t seed, size_t n, uint8_t *msg32, uint8_t *sig65,
+                   uint8_t *pub65, uint8_t *addr20);
+int gsv_synth_sign_dev(gsv_ctx *ctx, uint64_t seed, size_t n, uint8_t *d_msg32, uint8_t *d_sig65,
+                       uint8_t *d_pub65, uint8_t *d_addr20, void *stream);
+
+/* ---- notary validation of whole collations (Cfg4) ----
+ * For each shard body: blob-deserialize (sharding/utils/marshal.go:144-198), RLP-decode each tx,
+ * recover every sender (EIP-155 signer with chain_id), and compute the chunk root.
+ * Outputs per shard: root32, tx count, and a validity bitmap of max_txs bits (bit t = tx t
+ * recovered OK); senders (optional) n_total x 20 B in shard order. */
+int gsv_notary_validate_shards(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off,
+                               size_t n_shards, const uint8_t *chain_id, size_t chain_id_len,
+                               uint32_t max_txs, uint8_t *root32_out, uint32_t *ntx_out,
+                               uint8_t *valid_bitmap_out, uint8_t *senders_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSV_H */

@@ -1,0 +1,59 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — the CPU oracle for the collation-validation hot path.
+ *
+ * A plain-C restatement of the reference algorithms, written for clarity, used
+ * only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * checker.  Never linked into, loaded by, or called from the product library
+ * (geth-sharding_amd/csrc -> libgsv.so).  Each function cites the reference
+ * file:line it restates.  Pinned against the reference's golden vectors and
+ * against the reference's own C code (oracle/_ref) in tests/test_oracle.py.
+ */
+#ifndef GSV_ORACLE_H
+#define GSV_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+/* status codes: identical values to include/gsv.h */
+enum {
+    OR_OK = 0,
+    OR_INVALID_MSG_LEN = 1,
+    OR_INVALID_SIG_LEN = 2,
+    OR_INVALID_RECID = 3,
+    OR_RECOVER_FAILED = 4,
+    OR_INVALID_SIG = 5,
+    OR_INVALID_CHAIN_ID = 6,
+    OR_INVALID_PUBKEY = 7,
+    OR_BAD_RLP = 8,
+    OR_BN_BAD_INPUT = 9,
+};
+
+void oracle_keccak256(const uint8_t *in, size_t len, uint8_t out[32]);
+void oracle_keccak256_batch(const uint8_t *data, const uint64_t *off, long n, uint8_t *out32);
+void oracle_keccakf1600(uint64_t st[25]);
+void oracle_keccak_sponge(const uint8_t *in, size_t len, int rate, uint8_t dsbyte, uint8_t *out,
+                          size_t outlen);
+
+int oracle_ecrecover(uint8_t pub65[65], const uint8_t sig65[65], const uint8_t msg32[32]);
+void oracle_ecrecover_batch(const uint8_t *msg32, const uint8_t *sig65, long n, uint8_t *pub65,
+                            uint8_t *status, int threads);
+int oracle_recover_plain(uint8_t addr20[20], const uint8_t sighash[32], const uint8_t *r, size_t rlen,
+                         const uint8_t *s, size_t slen, const uint8_t *v, size_t vlen, int homestead);
+int oracle_tx_sender(uint8_t addr20[20], const uint8_t *rlp, size_t len, const uint8_t *chain_id,
+                     size_t chain_id_len, int signer_kind);
+int oracle_tx_sighash(uint8_t out32[32], const uint8_t *rlp, size_t len, const uint8_t *chain_id,
+                      size_t chain_id_len, int signer_kind);
+
+void oracle_derive_sha_bytes(const uint8_t *body, size_t n, uint8_t root[32]);
+int oracle_trie_root(const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
+                     const uint64_t *voff, long n, uint8_t root[32]);
+long oracle_blob_serialize(const uint8_t *data, const uint64_t *off, const uint8_t *skip_evm, long n,
+                           uint8_t *out, long cap);
+long oracle_blob_deserialize(const uint8_t *data, size_t len, uint8_t *out, uint64_t *off,
+                             uint8_t *skip_evm, long max_blobs);
+
+int oracle_secp_pubkey(uint8_t pub65[65], const uint8_t seckey[32]);
+int oracle_secp_sign(uint8_t sig65[65], const uint8_t msg32[32], const uint8_t seckey[32],
+                     const uint8_t nonce32[32]);
+
+int oracle_bn256_pairing_check(const uint8_t *in, size_t len);
+#endif

@@ -1,0 +1,263 @@
+"""Generates the committed golden fixtures under tests/golden/ (run in the build container,
+where /root/reference and oracle/_ref/libgsvref.so exist; the GPU box only reads the JSON).
+
+Sources of truth, in order:
+  1. vectors copied (as data) from the reference's own tests, cited file:line;
+  2. outputs of the reference's own C code compiled by `make -C oracle ref`
+     (libsecp256k1 with geth's cgo defines + ext.h; ethash sha3.c);
+  3. outputs of our CPU restatement (oracle/liboracle.so) where the reference is Go-only
+     (trie / DeriveSha / chunk root), which tests/test_oracle.py pins against (1).
+
+    python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import sys
+import zlib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from oracle import oracle as O  # noqa: E402
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+N_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+P_FIELD = 2**256 - 2**32 - 977
+
+
+def dump(name, obj):
+    with open(os.path.join(OUT, name), "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+    print("wrote", name)
+
+
+def h(b):
+    return bytes(b).hex()
+
+
+def keccak_fixtures():
+    raw = open(os.path.join(REF, "crypto/sha3/testdata/keccakKats.json.deflate"), "rb").read()
+    kats = json.loads(zlib.decompress(raw, -15))["kats"]["SHA3-256"]
+    # crypto/sha3/sha3_test.go:79-117 uses these ShortMsgKAT vectors; keep byte-aligned ones
+    sha3 = [{"msg": k["message"].lower() if k["length"] else "", "digest": k["digest"].lower()}
+            for k in kats if k["length"] % 8 == 0]
+    R = O.ref()
+    rng = random.Random(1)
+    k256 = [{"msg": h(b"abc"), "digest": "4e03657aea45a94fc7d47ba826c8d667c0d1e6e33a64a036ec44f58fa12d6c45",
+             "source": "crypto/crypto_test.go:37-41"}]
+    import ctypes
+    for ln in [0, 1, 31, 32, 55, 56, 64, 100, 134, 135, 136, 137, 200, 271, 272, 273, 1000, 1100]:
+        m = bytes(rng.getrandbits(8) for _ in range(ln))
+        out = ctypes.create_string_buffer(32)
+        R.gsvref_keccak256(out, m, len(m))
+        k256.append({"msg": h(m), "digest": h(out.raw), "source": "ethash sha3.c (oracle/_ref)"})
+    dump("keccak.json", {"sha3_256_kats": sha3, "keccak256": k256})
+
+
+def _sig(r, s, v):
+    return r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([v])
+
+
+def ecrecover_fixtures():
+    import ctypes
+    R = O.ref()
+    rng = random.Random(2)
+    cases = []
+
+    def add(msg, sig, note):
+        pub = ctypes.create_string_buffer(65)
+        rc = R.gsvref_ecrecover(pub, sig, msg)
+        cases.append({"msg": h(msg), "sig": h(sig), "rc": rc, "pub": h(pub.raw) if rc == 1 else "",
+                      "note": note})
+
+    # crypto/signature_test.go:30-45 TestEcrecover
+    add(bytes.fromhex("ce0677bb30baa8cf067c88db9811f4333d131bf8bcf12fe7065d211dce971008"),
+        bytes.fromhex("90f27b8b488db00b00606796d2987f6a5f59ae62ea05effe84fef5b8b0e549984a691139ad57a3f0b906637673aa2f63d1f55cb1a69199d4009eea23ceaddc9301"),
+        "crypto/signature_test.go:30-45")
+    # libsecp256k1 recovery/tests_impl.h:209-300 edge cases
+    msg = b"This is a very secret message..."
+    sig64 = bytes([0x67, 0xCB, 0x28, 0x5F, 0x9C, 0xD1, 0x94, 0xE8, 0x40, 0xD6, 0x29, 0x39, 0x7A, 0xF5, 0x56, 0x96,
+                   0x62, 0xFD, 0xE4, 0x46, 0x49, 0x99, 0x59, 0x63, 0x17, 0x9A, 0x7D, 0xD1, 0x7B, 0xD2, 0x35, 0x32,
+                   0x4B, 0x1B, 0x7D, 0xF3, 0x4C, 0xE1, 0xF6, 0x8E, 0x69, 0x4F, 0xF6, 0xF1, 0x1A, 0xC7, 0x51, 0xDD,
+                   0x7D, 0xD7, 0x3E, 0x38, 0x7E, 0xE4, 0xFC, 0x86, 0x6E, 0x1B, 0xE8, 0xEC, 0xC7, 0xDD, 0x95, 0x57])
+    for rid in range(4):
+        add(msg, sig64 + bytes([rid]), f"tests_impl.h:264-271 sig64 recid {rid} (only 1 recovers)")
+    for rid in range(4):
+        add(msg, _sig(4, 4, rid), f"tests_impl.h:297-298 (r,s)=(4,4) recid {rid}")
+    add(msg, _sig(N_ORDER + 4 - 2**256 if False else N_ORDER, 4, 0), "r == n (overflow) fails")
+    add(msg, _sig(4, N_ORDER, 0), "s == n (overflow) fails")
+    add(msg, _sig(0, 4, 0), "r == 0 fails")
+    add(msg, _sig(4, 0, 0), "s == 0 fails")
+    add(msg, _sig(2**256 - 1, 4, 1), "r = 2^256-1 fails")
+    pmn = P_FIELD - N_ORDER
+    for rid in (2, 3):
+        add(msg, _sig(pmn, 4, rid), f"r == p-n with recid {rid} fails")
+        add(msg, _sig(pmn - 1, 4, rid), f"r == p-n-1 with recid {rid}")
+    for rid in (4, 5, 27, 255):
+        add(msg, _sig(4, 4, rid), f"recid {rid} -> invalid recovery id")
+    # message >= n and == 0
+    add(b"\xff" * 32, _sig(4, 4, 0), "msg > n reduced mod n")
+    add(N_ORDER.to_bytes(32, "big"), _sig(4, 4, 1), "msg == n -> m = 0")
+    add(b"\0" * 32, _sig(4, 4, 1), "msg == 0")
+    # Q == infinity: R = k G, m = s*k mod n gives s R == m G  ->  recovery fails
+    for t in range(3):
+        while True:
+            k = rng.randrange(1, N_ORDER)
+            pub = ctypes.create_string_buffer(65)
+            R.gsvref_pubkey(pub, k.to_bytes(32, "big"))
+            x = int.from_bytes(pub.raw[1:33], "big")
+            y = int.from_bytes(pub.raw[33:65], "big")
+            if x < N_ORDER:
+                break
+        s = rng.randrange(1, N_ORDER)
+        m = s * k % N_ORDER
+        add(m.to_bytes(32, "big"), _sig(x, s, y & 1), "s R == m G -> Q at infinity")
+    # random RFC6979 signatures by libsecp256k1 (recid 0/1), plus tampered variants
+    for t in range(160):
+        key = rng.randrange(1, N_ORDER).to_bytes(32, "big")
+        m = bytes(rng.getrandbits(8) for _ in range(32))
+        sig = ctypes.create_string_buffer(65)
+        assert R.gsvref_sign(sig, m, key) == 1
+        sig = sig.raw
+        add(m, sig, "libsecp256k1 RFC6979 signature")
+        if t % 4 == 0:
+            add(m, sig[:64] + bytes([sig[64] ^ 1]), "recid flipped")
+        if t % 4 == 1:
+            s_hi = N_ORDER - int.from_bytes(sig[32:64], "big")
+            add(m, sig[:32] + s_hi.to_bytes(32, "big") + bytes([sig[64] ^ 1]), "high-s twin (valid for ecrecover)")
+        if t % 4 == 2:
+            add(m, sig[:64] + bytes([sig[64] | 2]), "recid | 2 (x = r + n)")
+    # random garbage (about half the x are non-residues)
+    for t in range(80):
+        r = rng.randrange(1, N_ORDER)
+        s = rng.randrange(1, N_ORDER)
+        m = bytes(rng.getrandbits(8) for _ in range(32))
+        add(m, _sig(r, s, rng.randrange(4)), "random r,s")
+    # small r with recid >= 2 (x = r + n < p)
+    for t in range(8):
+        r = rng.randrange(1, pmn)
+        add(bytes(rng.getrandbits(8) for _ in range(32)), _sig(r, rng.randrange(1, N_ORDER), 2 + (t & 1)),
+            "r < p-n, recid>=2")
+    dump("ecrecover.json", {"cases": cases})
+
+
+def tx_fixtures():
+    import ctypes
+    R = O.ref()
+    eip155 = [  # core/types/transaction_signing_test.go:74-101 (chainId 1)
+        ("f864808504a817c800825208943535353535353535353535353535353535353535808025a0044852b2a670ade5407e78fb2863c51de9fcb96542a07186fe3aeda6bb8a116da0044852b2a670ade5407e78fb2863c51de9fcb96542a07186fe3aeda6bb8a116d", "f0f6f18bca1b28cd68e4357452947e021241e9ce"),
+        ("f864018504a817c80182a410943535353535353535353535353535353535353535018025a0489efdaa54c0f20c7adf612882df0950f5a951637e0307cdcb4c672f298b8bcaa0489efdaa54c0f20c7adf612882df0950f5a951637e0307cdcb4c672f298b8bc6", "23ef145a395ea3fa3deb533b8a9e1b4c6c25d112"),
+        ("f864028504a817c80282f618943535353535353535353535353535353535353535088025a02d7c5bef027816a800da1736444fb58a807ef4c9603b7848673f7e3a68eb14a5a02d7c5bef027816a800da1736444fb58a807ef4c9603b7848673f7e3a68eb14a5", "2e485e0c23b4c3c542628a5f672eeab0ad4888be"),
+        ("f865038504a817c803830148209435353535353535353535353535353535353535351b8025a02a80e1ef1d7842f27f2e6be0972bb708b9a135c38860dbe73c27c3486c34f4e0a02a80e1ef1d7842f27f2e6be0972bb708b9a135c38860dbe73c27c3486c34f4de", "82a88539669a3fd524d669e858935de5e5410cf0"),
+        ("f865048504a817c80483019a28943535353535353535353535353535353535353535408025a013600b294191fc92924bb3ce4b969c1e7e2bab8f4c93c3fc6d0a51733df3c063a013600b294191fc92924bb3ce4b969c1e7e2bab8f4c93c3fc6d0a51733df3c060", "f9358f2538fd5ccfeb848b64a96b743fcc930554"),
+        ("f865058504a817c8058301ec309435353535353535353535353535353535353535357d8025a04eebf77a833b30520287ddd9478ff51abbdffa30aa90a8d655dba0e8a79ce0c1a04eebf77a833b30520287ddd9478ff51abbdffa30aa90a8d655dba0e8a79ce0c1", "a8f7aba377317440bc5b26198a363ad22af1f3a4"),
+        ("f866068504a817c80683023e3894353535353535353535353535353535353535353581d88025a06455bf8ea6e7463a1046a0b52804526e119b4bf5136279614e0b1e8e296a4e2fa06455bf8ea6e7463a1046a0b52804526e119b4bf5136279614e0b1e8e296a4e2d", "f1f571dc362a0e5b2696b8e775f8491d3e50de35"),
+        ("f867078504a817c807830290409435353535353535353535353535353535353535358201578025a052f1a9b320cab38e5da8a8f97989383aab0a49165fc91c737310e4f7e9821021a052f1a9b320cab38e5da8a8f97989383aab0a49165fc91c737310e4f7e9821021", "d37922162ab7cea97c97a87551ed02c9a38b7332"),
+        ("f867088504a817c8088302e2489435353535353535353535353535353535353535358202008025a064b1702d9298fee62dfeccc57d322a463ad55ca201256d01f62b45b2e1c21c12a064b1702d9298fee62dfeccc57d322a463ad55ca201256d01f62b45b2e1c21c10", "9bddad43f934d313c2b79ca28a432dd2b7281029"),
+        ("f867098504a817c809830334509435353535353535353535353535353535353535358202d98025a052f8f61201b2b11a78d6e866abc9c3db2ae8631fa656bfe5cb53668255367afba052f8f61201b2b11a78d6e866abc9c3db2ae8631fa656bfe5cb53668255367afb", "3c24d7329e92f84f08556ceb6df1cdb0104ca49f"),
+    ]
+    # core/types/transaction_test.go:88-125: HomesteadSigner senders = address of test key 45a915e4...
+    key = bytes.fromhex("45a915e4d060149eb4365960e6a7a45f334393093061116b197e3240065ff2d8")
+    pub = ctypes.create_string_buffer(65)
+    R.gsvref_pubkey(pub, key)
+    out = ctypes.create_string_buffer(32)
+    R.gsvref_keccak256(out, pub.raw[1:], 64)
+    test_addr = out.raw[12:].hex()
+    homestead = [
+        ("f8498080808080011ca09b16de9d5bdee2cf56c28d16275a4da68cd30273e2525f3959f5d62557489921a0372ebd8fb3345f7db7b5a86d42e24d36e983e259b0664ceb8c227ec9af572f3d", test_addr, "transaction_test.go:88-104 TestRecipientEmpty"),
+        ("f85d80808094000000000000000000000000000000000000000080011ca0527c0d8f5c63f7b9f41324a7c8a563ee1190bcbf0dac8ab446291bdbf32f5c79a0552c4ef0a09a04395074dab9ed34d3fbfb843c2f2546cc30fe89ec143ca94ca6", test_addr, "transaction_test.go:106-125 TestRecipientNormal"),
+    ]
+    # core/types/transaction_test.go:54-72: sighash + encoding of rightvrsTx (HomesteadSigner)
+    sighash = [("f86103018207d094b94f5374fce5edbc8e2a8697c15331677e6ebf0b0a8255441ca098ff921201554726367d2be8c804a7ff89ccf285ebc57dff8ae4c44b9c19ac4aa08887321be575c8095f789dd4c743dfe42c1820f9231f98a962b210e3ac2452a3",
+                "fe7a79529ed5f7c3375d06b26b186a8644e0e16c373d7a12be41c62d6042b77a", "transaction_test.go:54-72 rightvrsTx")]
+    dump("tx.json", {"eip155_chain1": [{"rlp": r, "addr": a} for r, a in eip155],
+                     "homestead": [{"rlp": r, "addr": a, "source": s} for r, a, s in homestead],
+                     "homestead_sighash": [{"rlp": r, "sighash": hh, "source": s} for r, hh, s in sighash]})
+
+
+def trie_fixtures():
+    # trie/trie_test.go:154-178 TestInsert
+    trie = [
+        {"pairs": [["doe", "reindeer"], ["dog", "puppy"], ["dogglesworth", "cat"]],
+         "root": "8aad789dff2f538bca5d8ea56e8abe10f4c7ba3a5dea95fea4cd6e7c3a1168d3", "source": "trie/trie_test.go:154-166"},
+        {"pairs": [["A", "a" * 50]],
+         "root": "d23786fb4a010da3ce639d66d5e904a11dbc02746d1ce25029e53290cabf28ab", "source": "trie/trie_test.go:168-178"},
+    ]
+    # core/types/block_test.go:29: header TxHash of SimpleTx = DeriveSha([tx]), tx from the block RLP
+    tx_rlp = "f85f800a82c35094095e7baea6a6c7c4c2dfeb977efac326af552d870a801ba09bea4c4daac7c7c52e093e6a4c35dbbcf8856f1af7b059ba20253e70848d094fa08a8fae537ce25ed8cb5af9adac3f141af69bd515bd2ba031522df09b97dd72b1"
+    derive = [{"items": [tx_rlp], "root": "5fe50b260da6308036625b850b5d6ced6d0a9f814c0688bc91ffb7b7a3a54b67",
+               "source": "core/types/block_test.go:29 (TxHash of SimpleTx)"}]
+    dump("trie.json", {"trie": trie, "derive_sha": derive,
+                       "empty_root": "56e81f171bcc55a6ff8345e692c0f86e5b48e01b996cadc001622fb5e363b421"})
+
+
+def xoshiro_bytes(seed: int, n: int) -> bytes:
+    """xoshiro256** byte stream (SURVEY.md §8d body generator), splitmix64-seeded."""
+    import numpy as np
+    M = (1 << 64) - 1
+
+    def splitmix(x):
+        x = (x + 0x9E3779B97F4A7C15) & M
+        z = x
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return x, z ^ (z >> 31)
+    x = seed
+    s = []
+    for _ in range(4):
+        x, z = splitmix(x)
+        s.append(z)
+    out = bytearray()
+    rotl = lambda v, k: ((v << k) | (v >> (64 - k))) & M
+    while len(out) < n:
+        res = (rotl((s[1] * 5) & M, 7) * 9) & M
+        t = (s[1] << 17) & M
+        s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3]; s[2] ^= t; s[3] = rotl(s[3], 45)
+        out += res.to_bytes(8, "little")
+    return bytes(out[:n])
+
+
+def chunk_root_fixtures():
+    sizes = [1, 2, 15, 16, 17, 31, 32, 127, 128, 129, 255, 256, 257, 4095, 4096, 4097, 65535, 65536, 65537]
+    fills = {"random": None, "zero": 0x00, "7f": 0x7F, "80": 0x80, "ff": 0xFF}
+    rng = random.Random(3)
+    cases = []
+    for n in sizes:
+        for name, v in fills.items():
+            if v is None:
+                body = bytes(rng.getrandbits(8) for _ in range(n))
+            else:
+                body = bytes([v]) * n
+            # store small bodies inline; large ones by generator (seed) to keep fixtures small
+            case = {"n": n, "fill": name, "root": h(O.derive_sha_bytes(body))}
+            if v is None:
+                case["body"] = h(body) if n <= 4096 else None
+                if n > 4096:
+                    seed = rng.getrandbits(32)
+                    body = xoshiro_bytes(seed, n)
+                    case["xoshiro_seed"] = seed
+                    case["root"] = h(O.derive_sha_bytes(body))
+            cases.append(case)
+    # mixed small sizes with random content (inline)
+    for n in [3, 5, 7, 40, 100, 300, 1000, 2000]:
+        body = bytes(rng.getrandbits(8) for _ in range(n))
+        cases.append({"n": n, "fill": "random", "body": h(body), "root": h(O.derive_sha_bytes(body))})
+    # one full 2^20 body by generator
+    seed = 7
+    body = xoshiro_bytes(seed, 1 << 20)
+    cases.append({"n": 1 << 20, "fill": "random", "body": None, "xoshiro_seed": seed,
+                  "root": h(O.derive_sha_bytes(body))})
+    dump("chunk_root.json", {"cases": cases, "empty_root": "56e81f171bcc55a6ff8345e692c0f86e5b48e01b996cadc001622fb5e363b421"})
+
+
+if __name__ == "__main__":
+    if not O.ref_available():
+        sys.exit("oracle/_ref/libgsvref.so missing: run `make -C oracle ref` first")
+    keccak_fixtures()
+    ecrecover_fixtures()
+    tx_fixtures()
+    trie_fixtures()
+    chunk_root_fixtures()

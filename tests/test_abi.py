@@ -1,0 +1,43 @@
+"""CPU tests of the drop-in boundary: libgsv.so loads (no GPU needed to dlopen) and exports
+every symbol include/gsv.h declares, with the ctypes signatures the package binds."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "gsv.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gsv_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_the_boundary():
+    syms = header_symbols()
+    for s in ["gsv_ecrecover_batch", "gsv_sender_batch", "gsv_tx_sender_batch", "gsv_keccak256_batch",
+              "gsv_chunk_root_batch", "gsv_bn256_pairing_check_batch", "gsv_notary_validate_shards"]:
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    from gsv import _lib
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in header_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    from gsv import _lib
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert set(header_symbols()) == bound
+
+
+def test_no_oracle_in_product_package():
+    pkg = os.path.join(ROOT, "geth-sharding_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".cuh", ".h", ".cpp")):
+                txt = open(os.path.join(dp, f), errors="ignore").read()
+                for bad in ("from oracle", "import oracle", "liboracle", "libgsvref", "oracle_"):
+                    assert bad not in txt, (f, bad)

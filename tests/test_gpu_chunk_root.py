@@ -1,0 +1,66 @@
+"""GPU parity: collation chunk roots (gsv_chunk_root_batch) vs the oracle MPT restatement and the
+committed fixtures (pinned transitively by the trie golden roots, tests/test_oracle.py)."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _xoshiro(seed, n):
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import xoshiro_bytes
+    return xoshiro_bytes(seed, n)
+
+
+def test_chunk_root_fixtures(ctx):
+    g = golden("chunk_root.json")
+    bodies, want = [], []
+    for c in g["cases"]:
+        if c.get("body"):
+            body = bytes.fromhex(c["body"])
+        elif c.get("xoshiro_seed") is not None:
+            body = _xoshiro(c["xoshiro_seed"], c["n"])
+        else:
+            v = {"zero": 0, "7f": 0x7F, "80": 0x80, "ff": 0xFF}[c["fill"]]
+            body = bytes([v]) * c["n"]
+        bodies.append(body)
+        want.append(c["root"])
+    bodies.append(b"")
+    want.append(g["empty_root"])
+    out = ctx.chunk_root_batch(bodies)
+    for i, w in enumerate(want):
+        assert bytes(out[i]).hex() == w, (i, len(bodies[i]))
+
+
+def test_chunk_root_every_small_length(ctx, oracle):
+    # every N in 1..600 plus a few shapes around group boundaries, random content
+    rng = random.Random(17)
+    ns = list(range(1, 601)) + [1000, 4095, 4096, 4097, 65535, 65536, 65537, 70000]
+    bodies = [bytes(rng.getrandbits(8) for _ in range(n)) for n in ns]
+    out = ctx.chunk_root_batch(bodies)
+    for i, b in enumerate(bodies):
+        assert bytes(out[i]) == oracle.derive_sha_bytes(b), len(b)
+
+
+def test_chunk_root_byte_classes(ctx, oracle):
+    # values 0 (-> 0x80), 1..127 (single byte), 128..255 (0x81 b) change leaf sizes and inlining
+    rng = random.Random(5)
+    bodies = []
+    for n in [5, 6, 7, 17, 33, 100, 300]:
+        for pal in ([0], [1, 127], [128, 255], [0, 200], [0, 5, 250]):
+            bodies.append(bytes(rng.choice(pal) for _ in range(n)))
+    out = ctx.chunk_root_batch(bodies)
+    for i, b in enumerate(bodies):
+        assert bytes(out[i]) == oracle.derive_sha_bytes(b)
+
+
+def test_chunk_root_too_large(ctx):
+    from gsv import GsvError
+    with pytest.raises(GsvError):
+        ctx.chunk_root_batch([b"\0" * ((1 << 20) + 1)])

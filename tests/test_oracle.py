@@ -1,0 +1,146 @@
+"""CPU tests: pin the oracle (our C restatement) against the reference's own golden vectors
+and against the reference's own C code (oracle/_ref) where that is built."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+N_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+def rlp_uint(i: int) -> bytes:
+    # rlp.Encode(uint(i)) (rlp/encode.go:390 writeUint)
+    if i == 0:
+        return b"\x80"
+    b = i.to_bytes((i.bit_length() + 7) // 8, "big")
+    if len(b) == 1 and b[0] < 0x80:
+        return b
+    return bytes([0x80 + len(b)]) + b
+
+
+def test_keccak_permutation_vs_sha3_kats(oracle):
+    # crypto/sha3/sha3_test.go:79-117 KATs (dsbyte 0x06) pin Keccak-f[1600]
+    kats = golden("keccak.json")["sha3_256_kats"]
+    assert len(kats) >= 200
+    for k in kats:
+        assert oracle.sha3_256(bytes.fromhex(k["msg"])).hex() == k["digest"]
+
+
+def test_keccak_permutation_vs_hashlib(oracle):
+    rng = random.Random(5)
+    for n in list(range(0, 300, 7)) + [135, 136, 137, 271, 272, 273]:
+        m = bytes(rng.getrandbits(8) for _ in range(n))
+        assert oracle.sha3_256(m) == hashlib.sha3_256(m).digest()
+
+
+def test_keccak256_golden(oracle):
+    for v in golden("keccak.json")["keccak256"]:
+        assert oracle.keccak256(bytes.fromhex(v["msg"])).hex() == v["digest"], v["source"]
+
+
+def test_ecrecover_golden(oracle):
+    for c in golden("ecrecover.json")["cases"]:
+        rc, pub = oracle.ecrecover(bytes.fromhex(c["msg"]), bytes.fromhex(c["sig"]))
+        assert rc == c["rc"], c["note"]
+        if rc == 1:
+            assert pub.hex() == c["pub"], c["note"]
+
+
+def test_ecrecover_vs_reference_random(oracle):
+    R = oracle.ref()
+    if R is None:
+        pytest.skip("reference build (oracle/_ref) not present")
+    import ctypes
+    rng = random.Random(11)
+    for _ in range(64):
+        key = rng.randrange(1, N_ORDER).to_bytes(32, "big")
+        m = bytes(rng.getrandbits(8) for _ in range(32))
+        sig = ctypes.create_string_buffer(65)
+        assert R.gsvref_sign(sig, m, key) == 1
+        pub = ctypes.create_string_buffer(65)
+        assert R.gsvref_ecrecover(pub, sig.raw, m) == 1
+        rc, mine = oracle.ecrecover(m, sig.raw)
+        assert rc == 1 and mine == pub.raw
+        # the oracle signer with an explicit nonce produces verifiable sigs too
+        k = rng.randrange(1, N_ORDER).to_bytes(32, "big")
+        s2 = oracle.secp_sign(m, key, k)
+        assert oracle.ecrecover(m, s2)[1] == oracle.secp_pubkey(key) == pub.raw
+
+
+def test_tx_sender_golden(oracle):
+    g = golden("tx.json")
+    for v in g["eip155_chain1"]:
+        st, addr = oracle.tx_sender(bytes.fromhex(v["rlp"]), 1, 0)
+        assert st == 0 and addr.hex() == v["addr"]
+        # wrong chain id -> ErrInvalidChainId
+        st, _ = oracle.tx_sender(bytes.fromhex(v["rlp"]), 2, 0)
+        assert st == 6
+    for v in g["homestead"]:
+        st, addr = oracle.tx_sender(bytes.fromhex(v["rlp"]), 0, 1)
+        assert st == 0 and addr.hex() == v["addr"], v["source"]
+        # an EIP155 signer falls back to Homestead for unprotected txs (V = 27/28)
+        st, addr = oracle.tx_sender(bytes.fromhex(v["rlp"]), 1, 0)
+        assert st == 0 and addr.hex() == v["addr"]
+    for v in g["homestead_sighash"]:
+        st, sh = oracle.tx_sighash(bytes.fromhex(v["rlp"]), 0, 1)
+        assert st == 0 and sh.hex() == v["sighash"], v["source"]
+
+
+def test_trie_golden(oracle):
+    g = golden("trie.json")
+    for t in g["trie"]:
+        pairs = [(k.encode(), v.encode()) for k, v in t["pairs"]]
+        assert oracle.trie_root(pairs).hex() == t["root"], t["source"]
+    for d in g["derive_sha"]:
+        pairs = [(rlp_uint(i), bytes.fromhex(x)) for i, x in enumerate(d["items"])]
+        assert oracle.trie_root(pairs).hex() == d["root"], d["source"]
+    assert oracle.derive_sha_bytes(b"").hex() == g["empty_root"]
+
+
+def test_derive_sha_bytes_matches_generic_trie(oracle):
+    # DeriveSha(Chunks(body)) == generic trie over (rlp(i), rlp(byte)) (derive_sha.go:32-41)
+    rng = random.Random(9)
+    for n in [1, 2, 16, 17, 127, 128, 129, 300, 1000]:
+        body = bytes(rng.getrandbits(8) for _ in range(n))
+        pairs = [(rlp_uint(i), rlp_uint(b)) for i, b in enumerate(body)]
+        assert oracle.trie_root(pairs) == oracle.derive_sha_bytes(body)
+
+
+def test_chunk_root_golden_small(oracle):
+    for c in golden("chunk_root.json")["cases"]:
+        if c.get("body"):
+            assert oracle.derive_sha_bytes(bytes.fromhex(c["body"])).hex() == c["root"]
+        elif c["fill"] != "random":
+            v = {"zero": 0, "7f": 0x7F, "80": 0x80, "ff": 0xFF}[c["fill"]]
+            if c["n"] <= 65537:
+                assert oracle.derive_sha_bytes(bytes([v]) * c["n"]).hex() == c["root"]
+
+
+def test_blob_codec_layout(oracle):
+    # sharding/utils/marshal_test.go:183-217 TestSerializeTestData
+    blob = bytes(range(60))
+    data = oracle.blob_serialize([blob])
+    assert len(data) == 64
+    assert data[32] == 0x1D and data[0] == 0
+    assert all(data[i] == i - 1 for i in range(1, 32))
+    assert all(data[i] == i - 2 for i in range(33, 62))
+    # round trip with mixed lengths and skipEvm flags
+    rng = random.Random(4)
+    blobs = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 200))) for _ in range(20)]
+    flags = [rng.randrange(2) for _ in blobs]
+    back = oracle.blob_deserialize(oracle.blob_serialize(blobs, flags))
+    assert [b for b, _ in back] == blobs
+    assert [f for _, f in back] == flags
+
+
+def test_oracle_batch_threads_agree(oracle):
+    rng = np.random.default_rng(0)
+    msgs = rng.integers(0, 256, (64, 32), dtype=np.uint8)
+    sigs = rng.integers(0, 256, (64, 65), dtype=np.uint8)
+    sigs[:, 64] = rng.integers(0, 4, 64)
+    p1, s1 = oracle.ecrecover_batch(msgs, sigs, threads=1)
+    p4, s4 = oracle.ecrecover_batch(msgs, sigs, threads=4)
+    assert (p1 == p4).all() and (s1 == s4).all()
