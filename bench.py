@@ -1,0 +1,259 @@
+"""Benchmark of the collation-validation hot path on MI355X (BASELINE.json metric:
+"ecrecover sigs/sec + Keccak collation GB/s").
+
+Default workload (BASELINE.json configs[1]): one step = recover 1,048,576 secp256k1 signatures and
+derive their Keccak-256 addresses on each GPU (inputs already resident in HBM), i.e. the
+crypto.Ecrecover / types.Sender hot path.  `value` = signatures recovered by all ranks / time.
+Weak scaling: every rank owns its own 2^20 signatures (independent units, no data-path
+collective).  The chunk-root leg (configs[2]: 100 shards x 1 MiB bodies) is measured in the same
+run and reported as `collation_GBps`.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ecrecover|chunk_root|notary]
+
+With N > 1 the driver launches one process per GPU via torch.distributed.run; rank 0 prints the
+one JSON line.  Timing: barrier + synchronize around exactly K steps, max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "geth-sharding_amd"))
+sys.path.insert(0, ROOT)
+
+N_SIGS = 1 << 20          # configs[1]
+N_SHARDS = 100            # configs[2]/[3]
+BODY = 1 << 20            # collation size limit (sharding/collation.go:45)
+# algorithmic work per recovery (reference algorithm counted on libsecp256k1):
+# 1,358 fe_mul x 64 + 1,729 fe_sqr x 36 + 301 scalar mul/sqr x 64 32x32-bit partial products
+MACS_PER_RECOVERY = 1358 * 64 + 1729 * 36 + 301 * 64
+# gfx950 v_mad_u64_u32 issue rate: half rate = 16 lanes/clk/SIMD (measured, profiles/r01_microbench_int.txt)
+PEAK_MAC = 256 * 4 * 16 * 2.4e9
+PERMS_PER_MIB = 83016      # Keccak-f permutations per 1 MiB chunk root (data-independent)
+HBM_PEAK_GBPS = 8000.0
+
+
+def dist_setup():
+    import torch
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return ws, rank, local
+
+
+def barrier(ws):
+    import torch
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, ws):
+    import torch
+    if ws == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline_ecrecover(msgs: np.ndarray, sigs: np.ndarray, threads: int):
+    """The reference's own libsecp256k1 path (oracle/_ref, geth cgo defines + ext.h) on the host
+    cores; falls back to our C restatement (oracle) if the reference build is absent."""
+    from oracle import oracle as O
+    n = msgs.shape[0]
+    R = O.ref()
+    kind = "reference" if R is not None else "port"
+    pub = np.zeros((n, 65), np.uint8)
+    u8 = ctypes.POINTER(ctypes.c_uint8)
+
+    def run(lo, hi):
+        m = np.ascontiguousarray(msgs[lo:hi])
+        s = np.ascontiguousarray(sigs[lo:hi])
+        p = np.zeros((hi - lo, 65), np.uint8)
+        if R is not None:
+            R.gsvref_ecrecover_many(p.ctypes.data_as(u8), s.ctypes.data_as(u8), m.ctypes.data_as(u8), hi - lo)
+        else:
+            st = np.zeros(hi - lo, np.uint8)
+            O.lib().oracle_ecrecover_batch(m.ctypes.data_as(u8), s.ctypes.data_as(u8), hi - lo,
+                                           p.ctypes.data_as(u8), st.ctypes.data_as(u8), 1)
+        pub[lo:hi] = p
+
+    if R is not None:
+        R.gsvref_init()
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=run, args=(n * t // threads, n * (t + 1) // threads)) for t in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    return n / dt, kind, pub
+
+
+def cpu_baseline_chunk_root(body: bytes, reps: int):
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        O.derive_sha_bytes(body)
+    dt = time.perf_counter() - t0
+    return reps * len(body) / dt / 1e9
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="ecrecover", choices=["ecrecover", "chunk_root"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-chunk-leg", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    ws, rank, local = dist_setup()
+    import gsv
+    from gsv import _lib
+    ctx = gsv.Context(local)
+    stream = torch.cuda.Stream()
+    dev = torch.device("cuda", local)
+
+    # ---------------------------------------------------------------- ecrecover leg (configs[1])
+    msg = torch.empty((N_SIGS, 32), dtype=torch.uint8, device=dev)
+    sig = torch.empty((N_SIGS, 65), dtype=torch.uint8, device=dev)
+    epub = torch.empty((N_SIGS, 65), dtype=torch.uint8, device=dev)
+    eaddr = torch.empty((N_SIGS, 20), dtype=torch.uint8, device=dev)
+    pub = torch.empty((N_SIGS, 65), dtype=torch.uint8, device=dev)
+    addr = torch.empty((N_SIGS, 20), dtype=torch.uint8, device=dev)
+    st = torch.empty((N_SIGS,), dtype=torch.uint8, device=dev)
+    with torch.cuda.stream(stream):
+        ctx.synth_sign_dev(1000 + rank, msg, sig, epub, eaddr, stream=stream)
+    stream.synchronize()
+
+    def step():
+        ctx.ecrecover_batch_dev(msg, sig, pub, addr, st, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    # size-independent parity property on the full batch: recover(sign(m, d)) == pub(d), addr(d)
+    assert int(st.max().item()) == 0, "recovery failed on valid signatures"
+    assert torch.equal(pub, epub) and torch.equal(addr, eaddr), "recovered keys differ from signers"
+
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    barrier(ws)
+    stream.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    stream.synchronize()
+    barrier(ws)
+    dt = max_over_ranks(time.perf_counter() - t0, ws)
+    ctx.set_timing(False)
+    k_ms, k_n = ctx.kernel_time(_lib.K_ECRECOVER)
+    k_avg_ms = max_over_ranks(k_ms / max(k_n, 1), ws)
+    sigs_per_s = ws * N_SIGS * args.steps / dt
+
+    # ---------------------------------------------------------------- chunk-root leg (configs[2])
+    chunk = None
+    if not args.no_chunk_leg:
+        rng = np.random.default_rng(99 + rank)
+        bodies = torch.from_numpy(rng.integers(0, 256, N_SHARDS * BODY, dtype=np.uint8)).to(dev)
+        h_off = np.arange(N_SHARDS + 1, dtype=np.uint64) * BODY
+        roots = torch.empty((N_SHARDS, 32), dtype=torch.uint8, device=dev)
+        csteps = max(2, args.steps // 2)
+        for _ in range(max(1, args.warmup)):
+            ctx.chunk_root_batch_dev(bodies, h_off, roots, stream=stream)
+        stream.synchronize()
+        ctx.reset_timing()
+        ctx.set_timing(True)
+        barrier(ws)
+        t1 = time.perf_counter()
+        for _ in range(csteps):
+            ctx.chunk_root_batch_dev(bodies, h_off, roots, stream=stream)
+        stream.synchronize()
+        barrier(ws)
+        cdt = max_over_ranks(time.perf_counter() - t1, ws)
+        ctx.set_timing(False)
+        leaf_ms, leaf_n = ctx.kernel_time(_lib.K_CHUNK_LEAF)
+        lvl_ms, lvl_n = ctx.kernel_time(_lib.K_CHUNK_LEVEL)
+        chunk = {
+            "collation_GBps": round(ws * N_SHARDS * BODY * csteps / cdt / 1e9, 3),
+            "shards": N_SHARDS * ws, "body_bytes": BODY, "ms_per_step": round(cdt / csteps * 1e3, 3),
+            "permutations_per_s": round(ws * N_SHARDS * PERMS_PER_MIB * csteps / cdt, 1),
+            "bottom_kernel_avg_ms": round(leaf_ms / max(leaf_n, 1), 4),
+            "level_kernels_ms_per_step": round(lvl_ms / csteps, 4),
+        }
+        # parity spot check of one shard against the oracle (outside the timed region)
+        if rank == 0:
+            from oracle import oracle as O
+            b0 = bodies[:BODY].cpu().numpy()
+            assert bytes(roots[0].cpu().numpy()) == O.derive_sha_bytes(b0), "chunk root mismatch vs oracle"
+
+    # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        sample = 4096 * threads
+        m_h = msg[:sample].cpu().numpy()
+        s_h = sig[:sample].cpu().numpy()
+        rate, kind, cpub = cpu_baseline_ecrecover(m_h, s_h, threads)
+        assert (cpub == epub[:sample].cpu().numpy()).all(), "CPU baseline disagrees with the GPU"
+        cpu = {"value": round(rate, 1), "unit": "sigs/s", "cores": threads, "kind": kind,
+               "sample": f"{sample} signatures of the same synthetic workload, "
+                         f"{'libsecp256k1 secp256k1_ext_ecdsa_recover (oracle/_ref)' if kind == 'reference' else 'oracle restatement'}"
+                         f", {threads} threads"}
+        if chunk is not None:
+            cbody = bodies[:BODY].cpu().numpy().tobytes()
+            chunk["cpu_collation_GBps_1core_oracle"] = round(cpu_baseline_chunk_root(cbody, 1), 4)
+
+    if rank == 0:
+        achieved = MACS_PER_RECOVERY * N_SIGS / (k_avg_ms * 1e-3)
+        line = {
+            "metric": "ecrecover sigs/sec + Keccak collation GB/s",
+            "value": round(sigs_per_s, 1),
+            "unit": "sigs/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (GPU-signed secp256k1 signatures, keccak-derived keys/msgs/nonces)",
+            "config": {"workload": "1M-signature secp256k1 ecrecover + Keccak-256 address derivation "
+                                   "per GPU (BASELINE.json configs[1])",
+                       "signatures_per_gpu": N_SIGS, "parallelism": f"shard-partitioned x{ws}"},
+            "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_MAC / 1e12, 3),
+                         "unit": "TMAC/s", "frac": round(achieved / PEAK_MAC, 4), "traffic": None,
+                         "kernel": "k_ecrecover", "kernel_avg_ms": round(k_avg_ms, 4),
+                         "algorithmic_per_unit": f"{MACS_PER_RECOVERY} 32x32-bit partial products per recovery"},
+            "cpu_baseline": cpu,
+        }
+        if chunk is not None:
+            line["collation_GBps"] = chunk["collation_GBps"]
+            line["chunk_root"] = chunk
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
