@@ -1,0 +1,580 @@
+// Batched BN254 PairingCheck on gfx950 (bn256.PairingCheck as driven by the bn256Pairing
+// precompile, core/vm/contracts.go:333-360; crypto/bn256/cloudflare/bn256.go:313-327).
+//
+// One lane per pair for decode + G2 subgroup check + Miller loop, one lane per check for the
+// product of Miller values + final exponentiation.  Three launches:
+//   k_bn_prepare  decode the 192-byte pair (bn256.go:120-164 G1.Unmarshal, :256-306 G2.Unmarshal):
+//                 coordinates < p, Montgomery encode, infinity detection, y^2 = x^3 + 3 on G1,
+//                 on-twist + Order*Q == infinity on G2 (twist.go:47-63)  -> pair status + points
+//   k_bn_miller   optimal-ate Miller loop (optate.go:122-210)             -> F_p^12 per pair
+//   k_bn_final    acc = prod of the check's Miller values (skipping infinity pairs),
+//                 finalExponentiation (optate.go:212-261), IsOne          -> verdict per check
+// HBM layout is structure-of-arrays, word-major ([word][pair]), so each lane's word loads and
+// stores coalesce across the wave.
+#include "bn254_dev.cuh"
+#include "gsv_internal.h"
+
+namespace gsv {
+namespace bn {
+
+// ---------------------------------------------------------------- F_p^12 (gfp12.go)
+GSV_DI void fp12_one(fp12& e) { fp6_zero(e.x); fp6_one(e.y); }
+GSV_DI bool fp12_is_one(const fp12& e) {
+    fp one;
+    fp_const(one, BN_ONE);
+    return fp2_is_zero(e.x.x) && fp2_is_zero(e.x.y) && fp2_is_zero(e.x.z) && fp2_is_zero(e.y.x) &&
+           fp2_is_zero(e.y.y) && fp_is_zero(e.y.z.x) && fp_eq(e.y.z.y, one);
+}
+GSV_DI void fp12_conj(fp12& e, const fp12& a) { fp6_neg(e.x, a.x); e.y = a.y; }
+// gfp12.go:60-66
+static BN_NI void fp12_frob_p(fp12* pe, const fp12* pa) {
+    const fp12 a = *pa;
+    fp12& e = *pe;
+    fp6 t;
+    fp6_frob(t, a.x);
+    fp6_frob(e.y, a.y);
+    fp2 k;
+    fp2_const(k, XI_P1_6_X, XI_P1_6_Y);
+    fp6_mul_fp2(e.x, t, k);
+}
+GSV_DI void fp12_frob(fp12& e, const fp12& a) { fp12_frob_p(&e, &a); }
+// gfp12.go:68-74
+static BN_NI void fp12_frob_p2_p(fp12* pe, const fp12* pa) {
+    const fp12 a = *pa;
+    fp12& e = *pe;
+    fp6 t;
+    fp6_frob_p2(t, a.x);
+    fp k;
+    fp_const(k, XI_PSQ1_6);
+    fp6_mul_fp(e.x, t, k);
+    fp6_frob_p2(e.y, a.y);
+}
+GSV_DI void fp12_frob_p2(fp12& e, const fp12& a) { fp12_frob_p2_p(&e, &a); }
+// gfp12.go:94-106
+static BN_NI void fp12_mul_p(fp12* pe, const fp12* pa, const fp12* pb) {
+    const fp12& a = *pa;
+    const fp12& b = *pb;
+    fp12& e = *pe;
+    fp6 tx, t, ty;
+    fp6_mul(tx, a.x, b.y);
+    fp6_mul(t, b.x, a.y);
+    fp6_add(tx, tx, t);
+    fp6_mul(ty, a.y, b.y);
+    fp6_mul(t, a.x, b.x);
+    fp6_mul_tau(t, t);
+    e.x = tx;
+    fp6_add(e.y, ty, t);
+}
+GSV_DI void fp12_mul(fp12& e, const fp12& a, const fp12& b) { fp12_mul_p(&e, &a, &b); }
+// gfp12.go:129-143
+static BN_NI void fp12_sqr_p(fp12* pe, const fp12* pa) {
+    const fp12 a = *pa;
+    fp12& e = *pe;
+    fp6 v0, t, ty;
+    fp6_mul(v0, a.x, a.y);
+    fp6_mul_tau(t, a.x);
+    fp6_add(t, a.y, t);
+    fp6_add(ty, a.x, a.y);
+    fp6_mul(ty, ty, t);
+    fp6_sub(ty, ty, v0);
+    fp6_mul_tau(t, v0);
+    fp6_sub(ty, ty, t);
+    fp6_add(e.x, v0, v0);
+    e.y = ty;
+}
+GSV_DI void fp12_sqr(fp12& e, const fp12& a) { fp12_sqr_p(&e, &a); }
+// gfp12.go:145-160
+GSV_DI void fp12_inv(fp12& e, const fp12& a) {
+    fp6 t1, t2;
+    fp6_sqr(t1, a.x);
+    fp6_sqr(t2, a.y);
+    fp6_mul_tau(t1, t1);
+    fp6_sub(t1, t2, t1);
+    fp6_inv(t2, t1);
+    fp6 nx;
+    fp6_neg(nx, a.x);
+    fp6_mul(e.x, nx, t2);
+    fp6_mul(e.y, a.y, t2);
+}
+// gfp12.go:113-127 with power = u (63 bits, top bit set)
+static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
+    fp12 sum = *a;  // the leading bit: 1^2 * a
+#pragma unroll 1
+    for (int i = 61; i >= 0; i--) {
+        fp12 t;
+        fp12_sqr(t, sum);
+        if ((BN_U >> i) & 1) fp12_mul(sum, t, *a);
+        else sum = t;
+    }
+    *c = sum;
+}
+
+// ---------------------------------------------------------------- twist points (twist.go)
+// twist.go:136-162 dbl-2009-l (t is not updated, as in the reference)
+static BN_NI void g2_double_p(g2j* pc, const g2j* pa) {
+    const g2j a = *pa;
+    g2j& c = *pc;
+    fp2 A, B, C, t, t2, d, e, f;
+    fp2_sqr(A, a.x);
+    fp2_sqr(B, a.y);
+    fp2_sqr(C, B);
+    fp2_add(t, a.x, B);
+    fp2_sqr(t2, t);
+    fp2_sub(t, t2, A);
+    fp2_sub(t2, t, C);
+    fp2_add(d, t2, t2);
+    fp2_add(t, A, A);
+    fp2_add(e, t, A);
+    fp2_sqr(f, e);
+    g2j r;
+    fp2_add(t, d, d);
+    fp2_sub(r.x, f, t);
+    fp2_add(t, C, C);
+    fp2_add(t2, t, t);
+    fp2_add(t, t2, t2);
+    fp2_sub(r.y, d, r.x);
+    fp2_mul(t2, e, r.y);
+    fp2_sub(r.y, t2, t);
+    fp2_mul(t, a.y, a.z);
+    fp2_add(r.z, t, t);
+    r.t = a.t;
+    c = r;
+}
+GSV_DI void g2_double(g2j& c, const g2j& a) { g2_double_p(&c, &a); }
+// twist.go:73-134 add-2007-bl with its infinity / doubling cases
+static BN_NI void g2_add_p(g2j* pc, const g2j* pa, const g2j* pb) {
+    const g2j a = *pa, b = *pb;
+    g2j& c = *pc;
+    if (fp2_is_zero(a.z)) { c = b; return; }
+    if (fp2_is_zero(b.z)) { c = a; return; }
+    fp2 z12, z22, u1, u2, t, s1, s2, h, i, j, r, v, t4, t6;
+    fp2_sqr(z12, a.z);
+    fp2_sqr(z22, b.z);
+    fp2_mul(u1, a.x, z22);
+    fp2_mul(u2, b.x, z12);
+    fp2_mul(t, b.z, z22);
+    fp2_mul(s1, a.y, t);
+    fp2_mul(t, a.z, z12);
+    fp2_mul(s2, b.y, t);
+    fp2_sub(h, u2, u1);
+    bool xeq = fp2_is_zero(h);
+    fp2_add(t, h, h);
+    fp2_sqr(i, t);
+    fp2_mul(j, h, i);
+    fp2_sub(t, s2, s1);
+    bool yeq = fp2_is_zero(t);
+    if (xeq && yeq) { g2_double(c, a); return; }
+    fp2_add(r, t, t);
+    fp2_mul(v, u1, i);
+    g2j o;
+    fp2_sqr(t4, r);
+    fp2_add(t, v, v);
+    fp2_sub(t6, t4, j);
+    fp2_sub(o.x, t6, t);
+    fp2_sub(t, v, o.x);
+    fp2_mul(t4, s1, j);
+    fp2_add(t6, t4, t4);
+    fp2_mul(t4, r, t);
+    fp2_sub(o.y, t4, t6);
+    fp2_add(t, a.z, b.z);
+    fp2_sqr(t4, t);
+    fp2_sub(t, t4, z12);
+    fp2_sub(t4, t, z22);
+    fp2_mul(o.z, t4, h);
+    o.t = a.t;
+    c = o;
+}
+GSV_DI void g2_add(g2j& c, const g2j& a, const g2j& b) { g2_add_p(&c, &a, &b); }
+// twist.go:47-63: y^2 == x^3 + 3/xi and Order * Q == infinity (twist.go:164-176 double-and-add)
+static BN_NI bool g2_in_subgroup(const g2a* q) {
+    fp2 y2, x3, b;
+    fp2_sqr(y2, q->y);
+    fp2_sqr(x3, q->x);
+    fp2_mul(x3, x3, q->x);
+    fp2_const(b, TWIST_B_X, TWIST_B_Y);
+    fp2_add(x3, x3, b);
+    if (!fp2_eq(y2, x3)) return false;
+    g2j a, sum;
+    a.x = q->x;
+    a.y = q->y;
+    fp2_one(a.z);
+    fp2_one(a.t);
+    // Order has bit length 254: the reference's loop starts at bit 254 (always 0) on the zero
+    // point; starting from sum = Q at bit 253 gives the same group element.
+    sum = a;
+#pragma unroll 1
+    for (int i = 252; i >= 0; i--) {
+        g2j t;
+        g2_double(t, sum);
+        if ((BN_ORDER[i >> 5] >> (i & 31)) & 1u) g2_add(sum, t, a);
+        else sum = t;
+    }
+    return fp2_is_zero(sum.z);
+}
+
+// ---------------------------------------------------------------- Miller loop (optate.go)
+// optate.go:3-50 (mixed addition r + p, p affine with t = 1; r2 = p.y^2)
+static BN_NI void line_add_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g2a* pp, const g1a* pq, const fp2* pr2) {
+    fp2& a = *pa;
+    fp2& b = *pb;
+    fp2& c = *pc;
+    g2j& r = *pr;
+    const g2a p = *pp;
+    const g1a q = *pq;
+    const fp2 r2 = *pr2;
+    fp2 B, D, H, I, E, J, L1, V, t, t2;
+    fp2_mul(B, p.x, r.t);
+    fp2_add(D, p.y, r.z);
+    fp2_sqr(D, D);
+    fp2_sub(D, D, r2);
+    fp2_sub(D, D, r.t);
+    fp2_mul(D, D, r.t);
+    fp2_sub(H, B, r.x);
+    fp2_sqr(I, H);
+    fp2_add(E, I, I);
+    fp2_add(E, E, E);
+    fp2_mul(J, H, E);
+    fp2_sub(L1, D, r.y);
+    fp2_sub(L1, L1, r.y);
+    fp2_mul(V, r.x, E);
+    g2j o;
+    fp2_sqr(o.x, L1);
+    fp2_sub(o.x, o.x, J);
+    fp2_sub(o.x, o.x, V);
+    fp2_sub(o.x, o.x, V);
+    fp2_add(o.z, r.z, H);
+    fp2_sqr(o.z, o.z);
+    fp2_sub(o.z, o.z, r.t);
+    fp2_sub(o.z, o.z, I);
+    fp2_sub(t, V, o.x);
+    fp2_mul(t, t, L1);
+    fp2_mul(t2, r.y, J);
+    fp2_add(t2, t2, t2);
+    fp2_sub(o.y, t, t2);
+    fp2_sqr(o.t, o.z);
+    fp2_add(t, p.y, o.z);
+    fp2_sqr(t, t);
+    fp2_sub(t, t, r2);
+    fp2_sub(t, t, o.t);
+    fp2_mul(t2, L1, p.x);
+    fp2_add(t2, t2, t2);
+    fp2_sub(a, t2, t);
+    fp2_mul_fp(c, o.z, q.y);
+    fp2_add(c, c, c);
+    fp2_neg(b, L1);
+    fp2_mul_fp(b, b, q.x);
+    fp2_add(b, b, b);
+    r = o;
+}
+GSV_DI void line_add(fp2& a, fp2& b, fp2& c, g2j& r, const g2a& p, const g1a& q, const fp2& r2) {
+    line_add_p(&a, &b, &c, &r, &p, &q, &r2);
+}
+// optate.go:52-92
+static BN_NI void line_double_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g1a* pq) {
+    fp2& a = *pa;
+    fp2& b = *pb;
+    fp2& c = *pc;
+    g2j& r = *pr;
+    const g1a q = *pq;
+    fp2 A, B, C, D, E, G, t;
+    fp2_sqr(A, r.x);
+    fp2_sqr(B, r.y);
+    fp2_sqr(C, B);
+    fp2_add(D, r.x, B);
+    fp2_sqr(D, D);
+    fp2_sub(D, D, A);
+    fp2_sub(D, D, C);
+    fp2_add(D, D, D);
+    fp2_add(E, A, A);
+    fp2_add(E, E, A);
+    fp2_sqr(G, E);
+    g2j o;
+    fp2_sub(o.x, G, D);
+    fp2_sub(o.x, o.x, D);
+    fp2_add(o.z, r.y, r.z);
+    fp2_sqr(o.z, o.z);
+    fp2_sub(o.z, o.z, B);
+    fp2_sub(o.z, o.z, r.t);
+    fp2_sub(o.y, D, o.x);
+    fp2_mul(o.y, o.y, E);
+    fp2_add(t, C, C);
+    fp2_add(t, t, t);
+    fp2_add(t, t, t);
+    fp2_sub(o.y, o.y, t);
+    fp2_sqr(o.t, o.z);
+    fp2_mul(t, E, r.t);
+    fp2_add(t, t, t);
+    fp2_neg(b, t);
+    fp2_mul_fp(b, b, q.x);
+    fp2_add(a, r.x, E);
+    fp2_sqr(a, a);
+    fp2_sub(a, a, A);
+    fp2_sub(a, a, G);
+    fp2_add(t, B, B);
+    fp2_add(t, t, t);
+    fp2_sub(a, a, t);
+    fp2_mul(c, o.z, r.t);
+    fp2_add(c, c, c);
+    fp2_mul_fp(c, c, q.y);
+    r = o;
+}
+GSV_DI void line_double(fp2& a, fp2& b, fp2& c, g2j& r, const g1a& q) { line_double_p(&a, &b, &c, &r, &q); }
+// optate.go:94-112
+static BN_NI void mul_line(fp12* ret, const fp2* a, const fp2* b, const fp2* c) {
+    fp6 a2, t3, t2, rx;
+    fp2_zero(a2.x);
+    a2.y = *a;
+    a2.z = *b;
+    fp6_mul(a2, a2, ret->x);
+    fp6_mul_fp2(t3, ret->y, *c);
+    fp2_zero(t2.x);
+    t2.y = *a;
+    fp2_add(t2.z, *b, *c);
+    fp6_add(rx, ret->x, ret->y);
+    fp6_mul(rx, rx, t2);
+    fp6_sub(rx, rx, a2);
+    fp6_sub(rx, rx, t3);
+    ret->x = rx;
+    fp6_mul_tau(a2, a2);
+    fp6_add(ret->y, t3, a2);
+}
+
+// optate.go:122-210 for affine q (twist) and p (G1), neither at infinity
+GSV_DI void miller(fp12& ret, const g2a& A, const g1a& B) {
+    fp12_one(ret);
+    g2j r;
+    r.x = A.x;
+    r.y = A.y;
+    fp2_one(r.z);
+    fp2_one(r.t);
+    fp2 r2, a, b, c;
+    fp2_sqr(r2, A.y);
+    g2a mA;
+    mA.x = A.x;
+    fp2_neg(mA.y, A.y);
+#pragma unroll 1
+    for (int i = 64; i > 0; i--) {
+        line_double(a, b, c, r, B);
+        if (i != 64) fp12_sqr(ret, ret);
+        mul_line(&ret, &a, &b, &c);
+        uint64_t bit = 1ull << (i - 1);
+        if ((NAF_POS | NAF_NEG) & bit) {
+            line_add(a, b, c, r, (NAF_POS & bit) ? A : mA, B, r2);
+            mul_line(&ret, &a, &b, &c);
+        }
+    }
+    // Q1 = pi(Q), -Q2 = -pi^2(Q) (optate.go:168-209)
+    g2a q1, mq2;
+    fp2 k;
+    fp2_conj(q1.x, A.x);
+    fp2_const(k, XI_P1_3_X, XI_P1_3_Y);
+    fp2_mul(q1.x, q1.x, k);
+    fp2_conj(q1.y, A.y);
+    fp2_const(k, XI_P1_2_X, XI_P1_2_Y);
+    fp2_mul(q1.y, q1.y, k);
+    fp kk;
+    fp_const(kk, XI_PSQ1_3);
+    fp2_mul_fp(mq2.x, A.x, kk);
+    mq2.y = A.y;
+    fp2_sqr(r2, q1.y);
+    line_add(a, b, c, r, q1, B, r2);
+    mul_line(&ret, &a, &b, &c);
+    fp2_sqr(r2, mq2.y);
+    line_add(a, b, c, r, mq2, B, r2);
+    mul_line(&ret, &a, &b, &c);
+}
+
+// optate.go:212-261
+static BN_NI void final_exp(fp12* out, const fp12* in) {
+    fp12 t1, t2, fp1, fp2_, fp3, fu, fu2, fu3, y0, y1, y2, y3, y4, y5, y6, t0;
+    fp6_neg(t1.x, in->x);
+    t1.y = in->y;
+    fp12_inv(t2, *in);
+    fp12_mul(t1, t1, t2);
+    fp12_frob_p2(t2, t1);
+    fp12_mul(t1, t1, t2);
+    fp12_frob(fp1, t1);
+    fp12_frob_p2(fp2_, t1);
+    fp12_frob(fp3, fp2_);
+    fp12_exp_u(&fu, &t1);
+    fp12_exp_u(&fu2, &fu);
+    fp12_exp_u(&fu3, &fu2);
+    fp12_frob(y3, fu);
+    fp12 fu2p, fu3p;
+    fp12_frob(fu2p, fu2);
+    fp12_frob(fu3p, fu3);
+    fp12_frob_p2(y2, fu2);
+    fp12_mul(y0, fp1, fp2_);
+    fp12_mul(y0, y0, fp3);
+    fp12_conj(y1, t1);
+    fp12_conj(y5, fu2);
+    fp12_conj(y3, y3);
+    fp12_mul(y4, fu, fu2p);
+    fp12_conj(y4, y4);
+    fp12_mul(y6, fu3, fu3p);
+    fp12_conj(y6, y6);
+    fp12_sqr(t0, y6);
+    fp12_mul(t0, t0, y4);
+    fp12_mul(t0, t0, y5);
+    fp12_mul(t1, y3, y5);
+    fp12_mul(t1, t1, t0);
+    fp12_mul(t0, t0, y2);
+    fp12_sqr(t1, t1);
+    fp12_mul(t1, t1, t0);
+    fp12_sqr(t1, t1);
+    fp12_mul(t0, t1, y1);
+    fp12_mul(t1, t1, y0);
+    fp12_sqr(t0, t0);
+    fp12_mul(*out, t0, t1);
+}
+
+// ---------------------------------------------------------------- SoA helpers
+// field element k (of K per item) of item i in a [K*8 words][n] word-major array
+GSV_DI void soa_load(fp& r, const uint32_t* __restrict__ base, uint32_t n, uint32_t i, int k) {
+#pragma unroll
+    for (int w = 0; w < 8; w++) r.v[w] = base[(size_t)(k * 8 + w) * n + i];
+}
+GSV_DI void soa_store(uint32_t* __restrict__ base, uint32_t n, uint32_t i, int k, const fp& r) {
+#pragma unroll
+    for (int w = 0; w < 8; w++) base[(size_t)(k * 8 + w) * n + i] = r.v[w];
+}
+GSV_DI void fp12_load(fp12& e, const uint32_t* base, uint32_t n, uint32_t i) {
+    fp* f = (fp*)&e;
+#pragma unroll
+    for (int k = 0; k < 12; k++) soa_load(f[k], base, n, i, k);
+}
+GSV_DI void fp12_store(uint32_t* base, uint32_t n, uint32_t i, const fp12& e) {
+    const fp* f = (const fp*)&e;
+#pragma unroll
+    for (int k = 0; k < 12; k++) soa_store(base, n, i, k, f[k]);
+}
+
+// gfP.Unmarshal (gfp.go:61-78) + montEncode: big-endian bytes -> limbs; false if >= p
+GSV_DI bool fp_unmarshal(fp& r, const uint8_t* p) {
+    uint32_t x[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint8_t* q = p + 28 - 4 * i;
+        x[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+    bool ok = !fp_geq_p(x);
+    fp t, r2;
+#pragma unroll
+    for (int i = 0; i < 8; i++) t.v[i] = ok ? x[i] : 0u;
+    fp_const(r2, BN_R2);
+    fp_mul_c(r, t, r2);
+    return ok;
+}
+
+// ---------------------------------------------------------------- kernels
+enum : uint8_t { PS_OK = 0, PS_SKIP = 1, PS_BAD = 2 };
+
+__global__ __launch_bounds__(64) void k_bn_prepare(const uint8_t* __restrict__ in,
+                                                   const uint64_t* __restrict__ pair_src,
+                                                   uint32_t npairs, uint8_t* __restrict__ pstat,
+                                                   uint32_t* __restrict__ pts /* [48 words][npairs] */) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    const uint8_t* s = in + pair_src[i];
+    g1a P;
+    g2a Q;
+    bool ok = fp_unmarshal(P.x, s);
+    ok = fp_unmarshal(P.y, s + 32) && ok;
+    ok = fp_unmarshal(Q.x.x, s + 64) && ok;  // imaginary part first (bn256.go:267-278)
+    ok = fp_unmarshal(Q.x.y, s + 96) && ok;
+    ok = fp_unmarshal(Q.y.x, s + 128) && ok;
+    ok = fp_unmarshal(Q.y.y, s + 160) && ok;
+    bool inf1 = fp_is_zero(P.x) && fp_is_zero(P.y);
+    bool inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
+    if (ok && !inf1) {  // curve.go:39-52: y^2 == x^3 + 3
+        fp y2, x3, b;
+        fp_mul_c(y2, P.y, P.y);
+        fp_mul_c(x3, P.x, P.x);
+        fp_mul_c(x3, x3, P.x);
+        fp_const(b, BN_THREE);
+        fp_add(x3, x3, b);
+        ok = fp_eq(y2, x3);
+    }
+    if (ok && !inf2) ok = g2_in_subgroup(&Q);
+    pstat[i] = !ok ? PS_BAD : (inf1 || inf2) ? PS_SKIP : PS_OK;
+    soa_store(pts, npairs, i, 0, P.x);
+    soa_store(pts, npairs, i, 1, P.y);
+    soa_store(pts, npairs, i, 2, Q.x.x);
+    soa_store(pts, npairs, i, 3, Q.x.y);
+    soa_store(pts, npairs, i, 4, Q.y.x);
+    soa_store(pts, npairs, i, 5, Q.y.y);
+}
+
+__global__ __launch_bounds__(64) void k_bn_miller(const uint8_t* __restrict__ pstat,
+                                                  const uint32_t* __restrict__ pts, uint32_t npairs,
+                                                  uint32_t* __restrict__ fv /* [96 words][npairs] */) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    if (pstat[i] != PS_OK) return;
+    g1a P;
+    g2a Q;
+    soa_load(P.x, pts, npairs, i, 0);
+    soa_load(P.y, pts, npairs, i, 1);
+    soa_load(Q.x.x, pts, npairs, i, 2);
+    soa_load(Q.x.y, pts, npairs, i, 3);
+    soa_load(Q.y.x, pts, npairs, i, 4);
+    soa_load(Q.y.y, pts, npairs, i, 5);
+    fp12 f;
+    miller(f, Q, P);
+    fp12_store(fv, npairs, i, f);
+}
+
+__global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ check_first,
+                                                 uint32_t nchecks, const uint8_t* __restrict__ pstat,
+                                                 const uint32_t* __restrict__ fv, uint32_t npairs,
+                                                 uint8_t* __restrict__ verdict) {
+    uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchecks) return;
+    uint32_t b = check_first[c], e = check_first[c + 1];
+    bool bad = false, any = false;
+    fp12 acc;
+    fp12_one(acc);
+    for (uint32_t p = b; p < e; p++) {
+        uint8_t st = pstat[p];
+        bad = bad || st == PS_BAD;
+        if (st != PS_OK) continue;
+        fp12 f;
+        fp12_load(f, fv, npairs, p);
+        if (!any) acc = f;  // 1 * f == f exactly (canonical residues)
+        else fp12_mul(acc, acc, f);
+        any = true;
+    }
+    fp12 r;
+    final_exp(&r, &acc);
+    verdict[c] = bad ? GSV_PAIRING_BAD_INPUT : fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
+}
+
+}  // namespace bn
+
+hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
+                                const uint32_t* d_check_first, uint32_t nchecks, uint8_t* d_pstat,
+                                uint32_t* d_pts, uint32_t* d_fv, uint8_t* d_verdict, hipStream_t st,
+                                void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx) {
+    if (npairs) {
+        if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
+        hipLaunchKernelGGL(bn::k_bn_prepare, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
+                           d_pstat, d_pts);
+        if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
+        hipLaunchKernelGGL(bn::k_bn_miller, dim3((npairs + 63) / 64), dim3(64), 0, st, d_pstat, d_pts, npairs, d_fv);
+        if (timer_end) timer_end(tctx, GSV_K_PAIRING);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (nchecks) {
+        if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
+        hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_first, nchecks,
+                           d_pstat, d_fv, npairs, d_verdict);
+        if (timer_end) timer_end(tctx, GSV_K_BN_FINAL);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace gsv

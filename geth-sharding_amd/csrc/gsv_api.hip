@@ -591,6 +591,103 @@ int gsv_tx_sender_batch(gsv_ctx* c, const uint8_t* rlp, const uint64_t* off, siz
     return tx_sender_impl(c, rlp, off, n, chain_id, chain_id_len, signer_kind, addr20_out, status);
 }
 
+// ------------------------------------------------------------------ BN254 pairing check
+// Host tables for a batch: check c = in[off[c] .. off[c+1]); a length that is not a multiple of
+// 192 is errBadPairingInput (core/vm/contracts.go:336-338) and contributes no pairs.
+struct BnTables {
+    std::vector<uint64_t> pair_src;
+    std::vector<uint32_t> check_first;
+    std::vector<uint8_t> bad_len;
+};
+static int bn_tables(const uint64_t* off, size_t n, uint64_t base, BnTables& t) {
+    t.check_first.resize(n + 1);
+    t.bad_len.assign(n, 0);
+    size_t np = 0;
+    for (size_t c = 0; c < n; c++) {
+        if (off[c + 1] < off[c]) return GSV_E_INVALID_ARG;
+        uint64_t len = off[c + 1] - off[c];
+        if (len % 192) t.bad_len[c] = 1;
+        else np += len / 192;
+    }
+    if (np > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
+    t.pair_src.resize(np);
+    size_t k = 0;
+    for (size_t c = 0; c < n; c++) {
+        t.check_first[c] = (uint32_t)k;
+        if (t.bad_len[c]) continue;
+        for (uint64_t o = off[c]; o < off[c + 1]; o += 192) t.pair_src[k++] = o - base;
+    }
+    t.check_first[n] = (uint32_t)k;
+    return GSV_SUCCESS;
+}
+
+// enqueue the three pairing kernels; d_in already in HBM, tables from the host
+static int bn_run(gsv_ctx* c, const uint8_t* d_in, const BnTables& t, size_t n, uint8_t* d_verdict,
+                  hipStream_t st) {
+    size_t np = t.pair_src.size();
+    size_t need = al(np * 8 + 8) + al((n + 1) * 4) + al(np + 1) + al(np * 48 * 4 + 4) + al(np * 96 * 4 + 4);
+    int rc = work_reserve(c, need + 4096);
+    if (rc) return rc;
+    Carve cv(c->work);
+    uint64_t* d_src = cv.take<uint64_t>(np * 8 + 8);
+    uint32_t* d_first = cv.take<uint32_t>((n + 1) * 4);
+    uint8_t* d_pstat = cv.take<uint8_t>(np + 1);
+    uint32_t* d_pts = cv.take<uint32_t>(np * 48 * 4 + 4);
+    uint32_t* d_fv = cv.take<uint32_t>(np * 96 * 4 + 4);
+    if (np) HIPCHK(hipMemcpyAsync(d_src, t.pair_src.data(), np * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_first, t.check_first.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
+    c->cur_stream = st;
+    HIPCHK(gsv::launch_bn256_pairing(d_in, d_src, (uint32_t)np, d_first, (uint32_t)n, d_pstat, d_pts, d_fv,
+                                     d_verdict, st, hook_begin, hook_end, c));
+    // errBadPairingInput for ragged lengths overrides the kernel's verdict (those checks had no pairs)
+    static const uint8_t bad = GSV_PAIRING_BAD_INPUT;
+    for (size_t i = 0; i < n; i++)
+        if (t.bad_len[i]) HIPCHK(hipMemcpyAsync(d_verdict + i, &bad, 1, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // host tables must outlive the async copies
+    return GSV_SUCCESS;
+}
+
+int gsv_bn256_pairing_check_batch_dev(gsv_ctx* c, const uint8_t* d_in, const uint64_t* h_off, size_t n,
+                                      uint8_t* d_verdict, void* stream) {
+    if (!c || (n && (!h_off || !d_verdict))) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    if (n > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
+    BnTables t;
+    int rc = bn_tables(h_off, n, 0, t);
+    if (rc) return rc;
+    if (!t.pair_src.empty() && !d_in) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->wmu);
+    HIPCHK(hipSetDevice(c->device));
+    return bn_run(c, d_in, t, n, d_verdict, stream ? (hipStream_t)stream : c->stream);
+}
+
+int gsv_bn256_pairing_check_batch(gsv_ctx* c, const uint8_t* in, const uint64_t* off, size_t n, uint8_t* verdict) {
+    if (!c || (n && (!off || !verdict))) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    if (n > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
+    BnTables t;
+    int rc = bn_tables(off, n, off[0], t);
+    if (rc) return rc;
+    if (!t.pair_src.empty() && !in) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    size_t bytes = off[n] - off[0];
+    rc = arena_reserve(c, al(bytes + 8) + al(n));
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_in = cv.take<uint8_t>(bytes + 8);
+    uint8_t* d_v = cv.take<uint8_t>(n);
+    if (bytes) HIPCHK(hipMemcpyAsync(d_in, in + off[0], bytes, hipMemcpyHostToDevice, c->stream));
+    {
+        std::lock_guard<std::mutex> g2(c->wmu);
+        rc = bn_run(c, d_in, t, n, d_v, c->stream);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(verdict, d_v, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
 // ------------------------------------------------------------------ notary validation (Cfg4)
 int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n_shards,
                                const uint8_t* chain_id, size_t chain_id_len, uint32_t max_txs,

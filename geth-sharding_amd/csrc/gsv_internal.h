@@ -29,6 +29,13 @@ hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies,
                                   void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
                                   void* tctx);
 
+// bn256.hip: pair_src[p] = byte offset of pair p in d_in; pairs of check c are
+// [check_first[c], check_first[c+1]); workspaces: pstat[npairs], pts[48][npairs], fv[96][npairs] words
+hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
+                                const uint32_t* d_check_first, uint32_t nchecks, uint8_t* d_pstat,
+                                uint32_t* d_pts, uint32_t* d_fv, uint8_t* d_verdict, hipStream_t st,
+                                void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx);
+
 constexpr size_t GTAB_ENTRIES = 32 * 256;
 constexpr size_t GTAB_BYTES = GTAB_ENTRIES * 64;
 

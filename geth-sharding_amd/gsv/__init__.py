@@ -219,5 +219,28 @@ def _chunk_root_batch_dev(self, bodies_t, h_off, roots_t, stream=None):
                                                ctypes.c_void_p(roots_t.data_ptr()), sp))
 
 
+def _pairing_check_batch(self, inputs) -> np.ndarray:
+    """bn256Pairing precompile inputs (k x 192 bytes each) -> verdicts GSV_PAIRING_FALSE / TRUE /
+    BAD_INPUT (core/vm/contracts.go:333-360, crypto/bn256/cloudflare/bn256.go:313-327)."""
+    n = len(inputs)
+    out = np.zeros(n, np.uint8)
+    if n == 0:
+        return out
+    flat, off = _pack(inputs)
+    check(_lib.load().gsv_bn256_pairing_check_batch(self._h, _ptr(flat), _ptr(off), n, _ptr(out)))
+    return out
+
+
+def _pairing_check_batch_dev(self, in_t, h_off, verdict_t, stream=None):
+    """in_t: torch uint8 CUDA tensor with all checks; h_off: numpy uint64 offsets (n+1)."""
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    n = h_off.shape[0] - 1
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_bn256_pairing_check_batch_dev(self._h, ctypes.c_void_p(in_t.data_ptr()), _ptr(h_off),
+                                                        n, ctypes.c_void_p(verdict_t.data_ptr()), sp))
+
+
+Context.pairing_check_batch = _pairing_check_batch
+Context.pairing_check_batch_dev = _pairing_check_batch_dev
 Context.chunk_root_batch = _chunk_root_batch
 Context.chunk_root_batch_dev = _chunk_root_batch_dev

@@ -38,6 +38,8 @@ K_CHUNK_LEAF = 2
 K_CHUNK_LEVEL = 3
 K_PAIRING = 4
 K_SENDER_PREP = 5
+K_BN_PREPARE = 6
+K_BN_FINAL = 7
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -65,6 +67,7 @@ SIGNATURES = [
     ("gsv_chunk_root_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
     ("gsv_chunk_root_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("gsv_bn256_pairing_check_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    ("gsv_bn256_pairing_check_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("gsv_synth_sign", ctypes.c_int, [_vp, ctypes.c_uint64, _sz, _vp, _vp, _vp, _vp]),
     ("gsv_synth_sign_dev", ctypes.c_int, [_vp, ctypes.c_uint64, _sz, _vp, _vp, _vp, _vp, _vp]),
     ("gsv_notary_validate_shards", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, ctypes.c_uint32,

@@ -95,6 +95,8 @@ int gsv_ctx_set_timing(gsv_ctx *ctx, int enable);
 #define GSV_K_CHUNK_LEVEL 3
 #define GSV_K_PAIRING 4
 #define GSV_K_SENDER_PREP 5
+#define GSV_K_BN_PREPARE 6 /* pair decode + G1 curve + G2 subgroup checks */
+#define GSV_K_BN_FINAL 7   /* per-check product + final exponentiation */
 #define GSV_K_COUNT 8
 /* total milliseconds and launch count accumulated for kernel `kid` since the last reset */
 int gsv_ctx_kernel_time(gsv_ctx *ctx, int kid, double *total_ms, long *launches);
@@ -146,6 +148,10 @@ int gsv_chunk_root_batch_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64
  * verdict[i] = GSV_PAIRING_TRUE / FALSE / BAD_INPUT. */
 int gsv_bn256_pairing_check_batch(gsv_ctx *ctx, const uint8_t *in, const uint64_t *off, size_t n,
                                   uint8_t *verdict);
+/* Device-resident form: d_in in HBM, h_off on the host (n+1 offsets into d_in), d_verdict in HBM.
+ * Enqueues on `stream` (NULL = the context stream); returns after the launches are queued. */
+int gsv_bn256_pairing_check_batch_dev(gsv_ctx *ctx, const uint8_t *d_in, const uint64_t *h_off, size_t n,
+                                      uint8_t *d_verdict, void *stream);
 
 /* ---- synthetic signed workload (bench / test data generator; signing is not on the path) ----
  * key_i, msg_i, nonce_i = Keccak256(le64(seed) || le64(i) || "key"/"msg"/"nce"), key and nonce

@@ -55,5 +55,11 @@ int oracle_secp_pubkey(uint8_t pub65[65], const uint8_t seckey[32]);
 int oracle_secp_sign(uint8_t sig65[65], const uint8_t msg32[32], const uint8_t seckey[32],
                      const uint8_t nonce32[32]);
 
+/* bn256_oracle.c: 1 true / 0 false / -1 error (core/vm/contracts.go:333-360) */
 int oracle_bn256_pairing_check(const uint8_t *in, size_t len);
+int oracle_bn256_miller(const uint8_t in192[192], uint8_t out384[384]);
+int oracle_bn256_final_exp(const uint8_t in384[384], uint8_t out384[384]);
+int oracle_bn256_g1_mul(uint8_t out64[64], const uint8_t *in64, const uint8_t k32[32]);
+int oracle_bn256_g2_mul(uint8_t out128[128], const uint8_t *in128, const uint8_t k32[32]);
+int oracle_bn256_g2_check(const uint8_t in128[128]);
 #endif

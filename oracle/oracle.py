@@ -59,8 +59,12 @@ def lib():
         L.oracle_blob_serialize.restype = ctypes.c_long
         L.oracle_blob_deserialize.argtypes = [c_u8p, ctypes.c_size_t, c_u8p, c_u64p, c_u8p, ctypes.c_long]
         L.oracle_blob_deserialize.restype = ctypes.c_long
-        if hasattr(L, "oracle_bn256_pairing_check"):
-            L.oracle_bn256_pairing_check.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_bn256_pairing_check.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_bn256_miller.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_bn256_final_exp.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_bn256_g1_mul.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_bn256_g2_mul.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_bn256_g2_check.argtypes = [ctypes.c_char_p]
         _LIB = L
     return _LIB
 
@@ -192,3 +196,27 @@ def blob_deserialize(data: bytes):
 def pairing_check(data: bytes):
     """1 true / 0 false / -1 bad input (core/vm/contracts.go:333-360 semantics)."""
     return lib().oracle_bn256_pairing_check(data, len(data))
+
+
+def bn256_g1_mul(k: int, point64: bytes | None = None):
+    """k * P in the precompile encoding (P = G1 generator when None); None on bad input."""
+    out = ctypes.create_string_buffer(64)
+    rc = lib().oracle_bn256_g1_mul(out, point64, (k % 2**256).to_bytes(32, "big"))
+    return None if rc else out.raw
+
+
+def bn256_g2_mul(k: int, point128: bytes | None = None):
+    """k * Q in the precompile encoding (Q = G2 generator when None); None on bad input."""
+    out = ctypes.create_string_buffer(128)
+    rc = lib().oracle_bn256_g2_mul(out, point128, (k % 2**256).to_bytes(32, "big"))
+    return None if rc else out.raw
+
+
+def bn256_g2_check(point128: bytes) -> bool:
+    return lib().oracle_bn256_g2_check(point128) == 0
+
+
+def bn256_miller(pair192: bytes):
+    out = ctypes.create_string_buffer(384)
+    rc = lib().oracle_bn256_miller(pair192, out)
+    return None if rc else out.raw

@@ -253,11 +253,78 @@ def chunk_root_fixtures():
     dump("chunk_root.json", {"cases": cases, "empty_root": "56e81f171bcc55a6ff8345e692c0f86e5b48e01b996cadc001622fb5e363b421"})
 
 
+def _precompiled_tests(var):
+    """(input, expected, name, line) rows of a precompiledTest table in core/vm/contracts_test.go"""
+    import re
+    src = open(os.path.join(REF, "core/vm/contracts_test.go")).read()
+    i = src.index("var " + var)
+    j = src.index("\n}\n", i)
+    rows = []
+    for m in re.finditer(r'input:\s*"([0-9a-f]*)",\s*expected:\s*"([0-9a-f]*)",\s*name:\s*"([^"]*)"', src[i:j]):
+        rows.append((m.group(1), m.group(2), m.group(3), src[:i + m.start()].count("\n") + 1))
+    return rows
+
+
+def bn256_fixtures():
+    """BN254 pairing-check verdicts (0 false / 1 true / 2 bad input, gsv.h GSV_PAIRING_*)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bn254_py as B
+    ref = [{"input": a, "verdict": int(e, 16), "name": n, "source": f"core/vm/contracts_test.go:{ln}"}
+           for a, e, n, ln in _precompiled_tests("bn256PairingTests")]
+    smul = [{"input": a, "expected": e, "name": n, "source": f"core/vm/contracts_test.go:{ln}"}
+            for a, e, n, ln in _precompiled_tests("bn256ScalarMulTests")]
+    rng = random.Random(4)
+    gen = []
+
+    def verdict(inp):
+        r = O.pairing_check(inp)
+        return 2 if r < 0 else r
+
+    def add(inp, note):
+        gen.append({"input": h(inp), "verdict": verdict(inp), "note": note})
+
+    def bilinear(a, b, c, d, perturb=0):
+        # e(aP, bQ) e(-abP, Q) e(cP, dQ) e(-cdP, Q) == 1
+        return (O.bn256_g1_mul(a) + O.bn256_g2_mul(b) + O.bn256_g1_mul(-a * b % B.R + perturb) +
+                O.bn256_g2_mul(1) + O.bn256_g1_mul(c) + O.bn256_g2_mul(d) + O.bn256_g1_mul(-c * d % B.R) +
+                O.bn256_g2_mul(1))
+
+    for k in range(6):
+        a, b, c, d = (rng.randrange(1, B.R) for _ in range(4))
+        add(bilinear(a, b, c, d), "4-pair bilinear identity (true)")
+        add(bilinear(a, b, c, d, perturb=1 + k), "4-pair bilinear identity, one scalar perturbed (false)")
+    g1, g2 = O.bn256_g1_mul(1), O.bn256_g2_mul(1)
+    inf1, inf2 = bytes(64), bytes(128)
+    add(inf1 + g2, "G1 infinity pair skipped (true)")
+    add(g1 + inf2, "G2 infinity pair skipped (true)")
+    add(inf1 + inf2 + g1 + g2, "infinity pair + one real pair (false)")
+    a = rng.randrange(1, B.R)
+    add(O.bn256_g1_mul(a) + g2 + inf1 + g2 + O.bn256_g1_mul(-a % B.R) + g2, "pair, infinity, inverse pair (true)")
+    pbytes = B.P.to_bytes(32, "big")
+    add(pbytes + g1[32:] + g2, "G1 x == p (bad)")
+    add(g1[:32] + (B.P + 5).to_bytes(32, "big") + g2, "G1 y > p (bad)")
+    add(g1[:32] + (3).to_bytes(32, "big") + g2, "G1 off curve (bad)")
+    for w in range(4):
+        q = bytearray(g2)
+        q[32 * w:32 * w + 32] = pbytes
+        add(g1 + bytes(q), f"G2 coordinate {w} == p (bad)")
+    qs = bytearray(g2)
+    qs[0:32], qs[32:64] = g2[32:64], g2[0:32]
+    add(g1 + bytes(qs), "G2 with real/imaginary parts swapped (off the twist, bad)")
+    off = B.twist_point_outside_g2(12345)
+    add(g1 + B.g2_encode(off), "G2 on the twist but not in the order-r subgroup (bad)")
+    add(g1 + g2 + g1 + B.g2_encode(B.twist_point_outside_g2(777)), "second pair outside G2 (bad)")
+    add(g1 + g2 + b"\x00", "length 193 (bad)")
+    add((g1 + g2)[:191], "length 191 (bad)")
+    add(b"", "empty input (true)")
+    dump("bn256.json", {"pairing": ref, "scalar_mul": smul, "generated": gen})
+
+
+FIXTURES = {"keccak": keccak_fixtures, "ecrecover": ecrecover_fixtures, "tx": tx_fixtures,
+            "trie": trie_fixtures, "chunk_root": chunk_root_fixtures, "bn256": bn256_fixtures}
+
 if __name__ == "__main__":
     if not O.ref_available():
         sys.exit("oracle/_ref/libgsvref.so missing: run `make -C oracle ref` first")
-    keccak_fixtures()
-    ecrecover_fixtures()
-    tx_fixtures()
-    trie_fixtures()
-    chunk_root_fixtures()
+    for name in (sys.argv[1:] or list(FIXTURES)):
+        FIXTURES[name]()

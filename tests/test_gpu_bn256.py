@@ -1,0 +1,92 @@
+"""GPU parity: batched BN254 PairingCheck (gsv_bn256_pairing_check_batch) vs the reference's
+precompile vectors (core/vm/contracts_test.go:279-337), the committed generated fixtures and the
+CPU oracle (oracle/bn256_oracle.c) on seeded random batches with ragged pair counts."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+
+
+def _v(oracle, inp):
+    r = oracle.pairing_check(inp)
+    return 2 if r < 0 else r
+
+
+def test_pairing_reference_vectors(ctx):
+    rows = golden("bn256.json")["pairing"]
+    out = ctx.pairing_check_batch([bytes.fromhex(r["input"]) for r in rows])
+    for i, r in enumerate(rows):
+        assert out[i] == r["verdict"], r["name"]
+
+
+def test_pairing_generated_fixtures(ctx):
+    rows = golden("bn256.json")["generated"]
+    out = ctx.pairing_check_batch([bytes.fromhex(r["input"]) for r in rows])
+    for i, r in enumerate(rows):
+        assert out[i] == r["verdict"], r["note"]
+
+
+def test_pairing_each_vector_alone(ctx):
+    # batch composition must not matter: every fixture on its own
+    rows = golden("bn256.json")["pairing"] + golden("bn256.json")["generated"]
+    for r in rows:
+        out = ctx.pairing_check_batch([bytes.fromhex(r["input"])])
+        assert out[0] == r["verdict"], r.get("name", r.get("note"))
+
+
+def test_pairing_random_batch_vs_oracle(ctx, oracle):
+    rng = random.Random(17)
+    g1 = [oracle.bn256_g1_mul(rng.randrange(1, R)) for _ in range(12)]
+    g2 = [oracle.bn256_g2_mul(rng.randrange(1, R)) for _ in range(6)]
+    inputs = []
+    for k in range(40):
+        kind = k % 4
+        if kind == 0:  # bilinear identity e(aP, bQ) e(-abP, Q) (true) or perturbed (false)
+            a, b = rng.randrange(1, R), rng.randrange(1, R)
+            pert = rng.choice([0, 0, 1])
+            inp = (oracle.bn256_g1_mul(a) + oracle.bn256_g2_mul(b) +
+                   oracle.bn256_g1_mul((-a * b + pert) % R) + oracle.bn256_g2_mul(1))
+        elif kind == 1:  # random pairs, ragged count 0..5, with infinities
+            inp = b""
+            for _ in range(rng.randrange(0, 6)):
+                p = rng.choice(g1 + [bytes(64)])
+                q = rng.choice(g2 + [bytes(128)])
+                inp += p + q
+        elif kind == 2:  # a malformed pair somewhere
+            pairs = [rng.choice(g1) + rng.choice(g2) for _ in range(rng.randrange(1, 4))]
+            bad = bytearray(rng.choice(pairs))
+            bad[rng.randrange(0, 192)] ^= 1 << rng.randrange(8)
+            pairs.insert(rng.randrange(0, len(pairs) + 1), bytes(bad))
+            inp = b"".join(pairs)
+        else:  # ragged byte length
+            inp = bytes(rng.getrandbits(8) for _ in range(rng.choice([1, 64, 191, 193, 383])))
+        inputs.append(inp)
+    out = ctx.pairing_check_batch(inputs)
+    want = np.array([_v(oracle, x) for x in inputs], np.uint8)
+    assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
+    assert set(want.tolist()) == {0, 1, 2}
+
+
+def test_pairing_empty_batch_and_empty_input(ctx):
+    assert ctx.pairing_check_batch([]).shape == (0,)
+    assert ctx.pairing_check_batch([b""])[0] == 1  # empty input -> true32Byte
+
+
+def test_precompile_run_semantics(ctx):
+    import gsv.bn256 as B
+    pre = B.Bn256Pairing()
+    rows = golden("bn256.json")["pairing"]
+    for r in rows:
+        assert pre.Run(bytes.fromhex(r["input"]), ctx) == (B.TRUE32 if r["verdict"] == 1 else B.FALSE32)
+    with pytest.raises(B.ErrBadPairingInput):
+        pre.Run(b"\x00" * 191, ctx)
+    bad = next(g for g in golden("bn256.json")["generated"] if "not in the order-r subgroup" in g["note"])
+    with pytest.raises(B.ErrMalformedPoint):
+        pre.Run(bytes.fromhex(bad["input"]), ctx)
+    assert pre.RequiredGas(b"\x00" * 384) == 100000 + 2 * 80000
