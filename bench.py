@@ -37,6 +37,7 @@ BODY = 1 << 20            # collation size limit (sharding/collation.go:45)
 MACS_PER_RECOVERY = 1358 * 64 + 1729 * 36 + 301 * 64
 # gfx950 v_mad_u64_u32 issue rate: half rate = 16 lanes/clk/SIMD (measured, profiles/r01_microbench_int.txt)
 PEAK_MAC = 256 * 4 * 16 * 2.4e9
+N_CHECKS = 65536           # configs[4]: 4-pair BN254 PairingCheck x 64k (split over the ranks)
 PERMS_PER_MIB = 83016      # Keccak-f permutations per 1 MiB chunk root (data-independent)
 HBM_PEAK_GBPS = 8000.0
 
@@ -122,6 +123,7 @@ def main():
     ap.add_argument("--workload", default="ecrecover", choices=["ecrecover", "chunk_root"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-chunk-leg", action="store_true")
+    ap.add_argument("--no-pairing-leg", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -205,6 +207,43 @@ def main():
             b0 = bodies[:BODY].cpu().numpy()
             assert bytes(roots[0].cpu().numpy()) == O.derive_sha_bytes(b0), "chunk root mismatch vs oracle"
 
+    # ---------------------------------------------------------------- pairing leg (configs[4])
+    pairing = None
+    if not args.no_pairing_leg:
+        nloc = N_CHECKS // ws + (1 if rank < N_CHECKS % ws else 0)
+        pin = torch.empty((nloc, 768), dtype=torch.uint8, device=dev)
+        pexp = torch.empty((nloc,), dtype=torch.uint8, device=dev)
+        pver = torch.empty((nloc,), dtype=torch.uint8, device=dev)
+        ctx.bn256_synth_checks_dev(5000 + rank, pin, pexp, stream=stream)
+        p_off = np.arange(nloc + 1, dtype=np.uint64) * 768
+        stream.synchronize()
+        ctx.pairing_check_batch_dev(pin, p_off, pver, stream=stream)  # warmup
+        stream.synchronize()
+        # size-independent parity property at full size: every verdict equals the generator's
+        assert torch.equal(pver, pexp), "pairing verdicts differ from the constructed truth"
+        psteps = 2
+        ctx.reset_timing()
+        ctx.set_timing(True)
+        barrier(ws)
+        t2 = time.perf_counter()
+        for _ in range(psteps):
+            ctx.pairing_check_batch_dev(pin, p_off, pver, stream=stream)
+        stream.synchronize()
+        barrier(ws)
+        pdt = max_over_ranks(time.perf_counter() - t2, ws)
+        ctx.set_timing(False)
+        k_prep, _ = ctx.kernel_time(_lib.K_BN_PREPARE)
+        k_mill, _ = ctx.kernel_time(_lib.K_PAIRING)
+        k_fin, _ = ctx.kernel_time(_lib.K_BN_FINAL)
+        pairing = {
+            "checks_per_s": round(N_CHECKS * psteps / pdt, 1), "checks": N_CHECKS, "pairs_per_check": 4,
+            "ms_per_step": round(pdt / psteps * 1e3, 3),
+            "prepare_kernel_ms": round(k_prep / psteps, 3), "miller_kernel_ms": round(k_mill / psteps, 3),
+            "final_exp_kernel_ms": round(k_fin / psteps, 3),
+            "verdicts": {"true": int((pexp == 1).sum().item()), "false": int((pexp == 0).sum().item()),
+                         "bad_input": int((pexp == 2).sum().item())},
+        }
+
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
@@ -221,6 +260,13 @@ def main():
         if chunk is not None:
             cbody = bodies[:BODY].cpu().numpy().tobytes()
             chunk["cpu_collation_GBps_1core_oracle"] = round(cpu_baseline_chunk_root(cbody, 1), 4)
+        if pairing is not None:
+            from oracle import oracle as O
+            hin = pin[:64].cpu().numpy()
+            t3 = time.perf_counter()
+            cv = [O.pairing_check(bytes(r)) for r in hin]
+            pairing["cpu_checks_per_s_1core_oracle"] = round(64 / (time.perf_counter() - t3), 1)
+            assert [2 if x < 0 else x for x in cv] == pexp[:64].cpu().tolist(), "pairing oracle disagrees"
 
     if rank == 0:
         achieved = MACS_PER_RECOVERY * N_SIGS / (k_avg_ms * 1e-3)
@@ -249,6 +295,8 @@ def main():
         if chunk is not None:
             line["collation_GBps"] = chunk["collation_GBps"]
             line["chunk_root"] = chunk
+        if pairing is not None:
+            line["bn256_pairing"] = pairing
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist

@@ -13,6 +13,7 @@
 // stores coalesce across the wave.
 #include "bn254_dev.cuh"
 #include "gsv_internal.h"
+#include "keccak_dev.cuh"
 
 namespace gsv {
 namespace bn {
@@ -549,7 +550,225 @@ __global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ ch
     verdict[c] = bad ? GSV_PAIRING_BAD_INPUT : fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
 }
 
+
+// ---------------------------------------------------------------- synthetic workload (bench data)
+// Not on the validation path.  Check i = e(aP, bQ) e(-bP, aQ) e(cP, dQ) e(-dP, cQ) == 1 with
+// a, b, c, d = Keccak-256(le64(seed) || le64(i) || tag) truncated to 253 bits (nonzero), P, Q the
+// G1 / G2 generators (curve.go:16-21, twist.go:20-32).  Every 8th check (i % 8 == 7) uses
+// -(d+1)P (false); every 1024th (i % 1024 == 1023) also corrupts a coordinate to p (bad input).
+__device__ constexpr uint32_t TWIST_GEN_XX[8] = {0xa84c6140u, 0xafb4737du, 0x5802d8c4u, 0x6043dd5au,
+                                                 0x52a02f86u, 0x09e950fcu, 0x3aea7b6bu, 0x14fef083u};
+__device__ constexpr uint32_t TWIST_GEN_XY[8] = {0x02bc2026u, 0x8e83b5d1u, 0x497b0172u, 0xdceb1935u,
+                                                 0x97811adfu, 0xfbb82647u, 0xaf96503bu, 0x19573841u};
+__device__ constexpr uint32_t TWIST_GEN_YX[8] = {0xc71856eeu, 0x64095b56u, 0x327d3cbbu, 0xdc57f922u,
+                                                 0x33351076u, 0x55f935beu, 0x93fd6482u, 0x0da4a0e6u};
+__device__ constexpr uint32_t TWIST_GEN_YY[8] = {0x886be9f6u, 0x619dfa9du, 0xf59e9b78u, 0xfe7fd297u,
+                                                 0x231b7dfeu, 0xff9e1a62u, 0xae9e4206u, 0x28fd7eebu};
+__device__ constexpr uint32_t BN_TWO[8] = {0x8b1e1b3au, 0xa6ba871bu, 0xeb8e167bu, 0x14f1d651u,
+                                           0xf0f28c58u, 0xccdd46deu, 0x340fbe5eu, 0x1c14ef83u};
+
+struct g1j { fp x, y, z; };
+// curve.go:143-172 dbl-2009-l
+static BN_NI void g1_double_p(g1j* pc, const g1j* pa) {
+    const g1j a = *pa;
+    fp A, B, C, t, t2, d, e, f;
+    fp_mul_c(A, a.x, a.x);
+    fp_mul_c(B, a.y, a.y);
+    fp_mul_c(C, B, B);
+    fp_add(t, a.x, B);
+    fp_mul_c(t2, t, t);
+    fp_sub(t, t2, A);
+    fp_sub(t2, t, C);
+    fp_add(d, t2, t2);
+    fp_add(t, A, A);
+    fp_add(e, t, A);
+    fp_mul_c(f, e, e);
+    g1j r;
+    fp_add(t, d, d);
+    fp_sub(r.x, f, t);
+    fp_add(t, C, C);
+    fp_add(t2, t, t);
+    fp_add(t, t2, t2);
+    fp_sub(r.y, d, r.x);
+    fp_mul_c(t2, e, r.y);
+    fp_sub(r.y, t2, t);
+    fp_mul_c(t, a.y, a.z);
+    fp_add(r.z, t, t);
+    *pc = r;
+}
+// curve.go:63-141 add-2007-bl
+static BN_NI void g1_add_p(g1j* pc, const g1j* pa, const g1j* pb) {
+    const g1j a = *pa, b = *pb;
+    if (fp_is_zero(a.z)) { *pc = b; return; }
+    if (fp_is_zero(b.z)) { *pc = a; return; }
+    fp z12, z22, u1, u2, t, s1, s2, h, i, j, r, v, t4, t6;
+    fp_mul_c(z12, a.z, a.z);
+    fp_mul_c(z22, b.z, b.z);
+    fp_mul_c(u1, a.x, z22);
+    fp_mul_c(u2, b.x, z12);
+    fp_mul_c(t, b.z, z22);
+    fp_mul_c(s1, a.y, t);
+    fp_mul_c(t, a.z, z12);
+    fp_mul_c(s2, b.y, t);
+    fp_sub(h, u2, u1);
+    bool xeq = fp_is_zero(h);
+    fp_add(t, h, h);
+    fp_mul_c(i, t, t);
+    fp_mul_c(j, h, i);
+    fp_sub(t, s2, s1);
+    bool yeq = fp_is_zero(t);
+    if (xeq && yeq) { g1_double_p(pc, pa); return; }
+    fp_add(r, t, t);
+    fp_mul_c(v, u1, i);
+    g1j o;
+    fp_mul_c(t4, r, r);
+    fp_add(t, v, v);
+    fp_sub(t6, t4, j);
+    fp_sub(o.x, t6, t);
+    fp_sub(t, v, o.x);
+    fp_mul_c(t4, s1, j);
+    fp_add(t6, t4, t4);
+    fp_mul_c(t4, r, t);
+    fp_sub(o.y, t4, t6);
+    fp_add(t, a.z, b.z);
+    fp_mul_c(t4, t, t);
+    fp_sub(t, t4, z12);
+    fp_sub(t4, t, z22);
+    fp_mul_c(o.z, t4, h);
+    *pc = o;
+}
+// k * P (k < 2^253 as 8 limbs, nonzero) -> affine Montgomery coordinates
+GSV_DI void g1_mul_gen(fp& ox, fp& oy, const uint32_t k[8]) {
+    g1j base, sum;
+    fp_const(base.x, BN_ONE);
+    fp_const(base.y, BN_TWO);
+    fp_const(base.z, BN_ONE);
+    fp_zero(sum.x);
+    fp_const(sum.y, BN_ONE);
+    fp_zero(sum.z);
+#pragma unroll 1
+    for (int b = 252; b >= 0; b--) {
+        g1j t;
+        g1_double_p(&t, &sum);
+        if ((k[b >> 5] >> (b & 31)) & 1u) g1_add_p(&sum, &t, &base);
+        else sum = t;
+    }
+    fp zi, zi2, zi3;
+    fp_inv(zi, sum.z);
+    fp_mul_c(zi2, zi, zi);
+    fp_mul_c(zi3, zi2, zi);
+    fp_mul_c(ox, sum.x, zi2);
+    fp_mul_c(oy, sum.y, zi3);
+}
+GSV_DI void g2_mul_gen(g2a& o, const uint32_t k[8]) {
+    g2j base, sum;
+    fp2_const(base.x, TWIST_GEN_XX, TWIST_GEN_XY);
+    fp2_const(base.y, TWIST_GEN_YX, TWIST_GEN_YY);
+    fp2_one(base.z);
+    fp2_one(base.t);
+    fp2_zero(sum.x);
+    fp2_one(sum.y);
+    fp2_zero(sum.z);
+    fp2_zero(sum.t);
+#pragma unroll 1
+    for (int b = 252; b >= 0; b--) {
+        g2j t;
+        g2_double(t, sum);
+        if ((k[b >> 5] >> (b & 31)) & 1u) g2_add(sum, t, base);
+        else sum = t;
+    }
+    fp2 zi, zi2, zi3;
+    fp2_inv(zi, sum.z);
+    fp2_sqr(zi2, zi);
+    fp2_mul(zi3, zi2, zi);
+    fp2_mul(o.x, sum.x, zi2);
+    fp2_mul(o.y, sum.y, zi3);
+}
+// montDecode + big-endian marshal (gfp.go:51-59)
+GSV_DI void fp_marshal(uint8_t* out, const fp& a) {
+    fp one, t;
+    fp_zero(one);
+    one.v[0] = 1;
+    fp_mul_c(t, a, one);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t w = t.v[7 - i];
+        out[4 * i] = (uint8_t)(w >> 24);
+        out[4 * i + 1] = (uint8_t)(w >> 16);
+        out[4 * i + 2] = (uint8_t)(w >> 8);
+        out[4 * i + 3] = (uint8_t)w;
+    }
+}
+GSV_DI void synth_scalar(uint32_t k[8], uint64_t seed, uint64_t i, uint32_t tag) {
+    uint64_t a[25];
+#pragma unroll
+    for (int j = 0; j < 25; j++) a[j] = 0;
+    a[0] = seed;
+    a[1] = i;
+    a[2] = (uint64_t)(tag & 0xFFFFFFu) | (0x01ull << 24);
+    a[16] = 0x8000000000000000ULL;
+    keccakf(a);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        k[2 * j] = (uint32_t)a[j];
+        k[2 * j + 1] = (uint32_t)(a[j] >> 32);
+    }
+    k[7] &= 0x1FFFFFFFu;  // < 2^253 < r
+    if ((k[0] | k[1] | k[2] | k[3] | k[4] | k[5] | k[6] | k[7]) == 0) k[0] = 1;
+}
+// one (G1, G2) pair of the check: lane (check, j) for j = 0..3
+__global__ __launch_bounds__(64) void k_bn_synth(uint64_t seed, uint32_t nchecks, uint8_t* __restrict__ out,
+                                                 uint8_t* __restrict__ expect) {
+    uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= nchecks * 4u) return;
+    uint32_t c = id >> 2, j = id & 3u;
+    uint32_t s1[8], s2[8];
+    // pair j: (x P, y Q) with (x, y) = (a, b), (-b, a), (c, d), (-d', c)
+    const uint32_t tags[4] = {0x61u, 0x62u, 0x63u, 0x64u};  // "a" "b" "c" "d"
+    uint32_t tx = (j == 0) ? tags[0] : (j == 1) ? tags[1] : (j == 2) ? tags[2] : tags[3];
+    uint32_t ty = (j == 0) ? tags[1] : (j == 1) ? tags[0] : (j == 2) ? tags[3] : tags[2];
+    synth_scalar(s1, seed, c, tx);
+    synth_scalar(s2, seed, c, ty);
+    bool is_false = (c % 8u) == 7u, is_bad = (c % 1024u) == 1023u;
+    if (j == 3 && is_false) {  // d + 1 (no overflow: d < 2^253)
+        uint32_t cy = 1;
+#pragma unroll
+        for (int w = 0; w < 8; w++) s1[w] = add_c(s1[w], 0u, cy);
+    }
+    fp px, py;
+    g1_mul_gen(px, py, s1);
+    if (j & 1u) fp_neg(py, py);  // -xP
+    g2a q;
+    g2_mul_gen(q, s2);
+    uint8_t* o = out + (size_t)c * 768 + j * 192;
+    fp_marshal(o, px);
+    fp_marshal(o + 32, py);
+    fp_marshal(o + 64, q.x.x);
+    fp_marshal(o + 96, q.x.y);
+    fp_marshal(o + 128, q.y.x);
+    fp_marshal(o + 160, q.y.y);
+    if (j == 2 && is_bad) {  // coordinate == p: bn256 "coordinate equals modulus"
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            uint32_t w = BN_P[7 - i];
+            o[4 * i] = (uint8_t)(w >> 24);
+            o[4 * i + 1] = (uint8_t)(w >> 16);
+            o[4 * i + 2] = (uint8_t)(w >> 8);
+            o[4 * i + 3] = (uint8_t)w;
+        }
+    }
+    if (j == 0 && expect)
+        expect[c] = is_bad ? GSV_PAIRING_BAD_INPUT : is_false ? GSV_PAIRING_FALSE : GSV_PAIRING_TRUE;
+}
+
 }  // namespace bn
+
+hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st) {
+    if (nchecks == 0) return hipSuccess;
+    uint32_t lanes = nchecks * 4u;
+    hipLaunchKernelGGL(bn::k_bn_synth, dim3((lanes + 63) / 64), dim3(64), 0, st, seed, nchecks, d_out, d_expect);
+    return hipGetLastError();
+}
 
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
                                 const uint32_t* d_check_first, uint32_t nchecks, uint8_t* d_pstat,

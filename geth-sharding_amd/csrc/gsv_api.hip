@@ -688,6 +688,14 @@ int gsv_bn256_pairing_check_batch(gsv_ctx* c, const uint8_t* in, const uint64_t*
     return GSV_SUCCESS;
 }
 
+int gsv_bn256_synth_checks_dev(gsv_ctx* c, uint64_t seed, size_t nchecks, uint8_t* d_out768, uint8_t* d_expect,
+                               void* stream) {
+    if (!c || (nchecks && !d_out768) || nchecks > 0x3FFFFFFFull) return GSV_E_INVALID_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    return hip_err(gsv::launch_bn256_synth(seed, (uint32_t)nchecks, d_out768, d_expect,
+                                           stream ? (hipStream_t)stream : c->stream));
+}
+
 // ------------------------------------------------------------------ notary validation (Cfg4)
 int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n_shards,
                                const uint8_t* chain_id, size_t chain_id_len, uint32_t max_txs,

@@ -36,6 +36,8 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                                 uint32_t* d_pts, uint32_t* d_fv, uint8_t* d_verdict, hipStream_t st,
                                 void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx);
 
+hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st);
+
 constexpr size_t GTAB_ENTRIES = 32 * 256;
 constexpr size_t GTAB_BYTES = GTAB_ENTRIES * 64;
 

@@ -240,6 +240,16 @@ def _pairing_check_batch_dev(self, in_t, h_off, verdict_t, stream=None):
                                                         n, ctypes.c_void_p(verdict_t.data_ptr()), sp))
 
 
+def _bn256_synth_checks_dev(self, seed, out_t, expect_t=None, stream=None):
+    """configs[4] synthetic 4-pair checks into out_t (torch uint8 CUDA, nchecks x 768)."""
+    n = out_t.shape[0]
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_bn256_synth_checks_dev(
+        self._h, ctypes.c_uint64(seed), n, ctypes.c_void_p(out_t.data_ptr()),
+        ctypes.c_void_p(expect_t.data_ptr()) if expect_t is not None else None, sp))
+
+
+Context.bn256_synth_checks_dev = _bn256_synth_checks_dev
 Context.pairing_check_batch = _pairing_check_batch
 Context.pairing_check_batch_dev = _pairing_check_batch_dev
 Context.chunk_root_batch = _chunk_root_batch

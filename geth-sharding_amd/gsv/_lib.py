@@ -68,6 +68,7 @@ SIGNATURES = [
     ("gsv_chunk_root_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("gsv_bn256_pairing_check_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
     ("gsv_bn256_pairing_check_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    ("gsv_bn256_synth_checks_dev", ctypes.c_int, [_vp, ctypes.c_uint64, _sz, _vp, _vp, _vp]),
     ("gsv_synth_sign", ctypes.c_int, [_vp, ctypes.c_uint64, _sz, _vp, _vp, _vp, _vp]),
     ("gsv_synth_sign_dev", ctypes.c_int, [_vp, ctypes.c_uint64, _sz, _vp, _vp, _vp, _vp, _vp]),
     ("gsv_notary_validate_shards", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, ctypes.c_uint32,
@@ -87,6 +88,13 @@ def load():
     global _lib
     with _lock:
         if _lib is None:
+            # PyTorch-ROCm ships its own libamdhip64; when both runtimes live in one process,
+            # torch's must initialise first or torch later finds no GPU.  Importing torch here (when
+            # installed) makes the order independent of what the caller imported first.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             if not os.path.exists(LIB_PATH):
                 raise OSError(f"libgsv.so not built at {LIB_PATH}: run `make -C geth-sharding_amd/csrc` "
                               "(or __graft_entry__.build()); there is no CPU fallback")

@@ -162,6 +162,13 @@ int gsv_synth_sign(gsv_ctx *ctx, uint64_t seed, size_t n, uint8_t *msg32, uint8_
 int gsv_synth_sign_dev(gsv_ctx *ctx, uint64_t seed, size_t n, uint8_t *d_msg32, uint8_t *d_sig65,
                        uint8_t *d_pub65, uint8_t *d_addr20, void *stream);
 
+/* ---- synthetic pairing workload (bench / test data; configs[4]) ----
+ * nchecks x 768 B precompile inputs: check i = e(aP,bQ) e(-bP,aQ) e(cP,dQ) e(-dP,cQ) (true) with
+ * a..d = Keccak256(le64(seed) || le64(i) || tag) mod 2^253; i % 8 == 7 perturbs d (false);
+ * i % 1024 == 1023 also sets a coordinate to p (bad input).  expect (optional) gets the verdicts. */
+int gsv_bn256_synth_checks_dev(gsv_ctx *ctx, uint64_t seed, size_t nchecks, uint8_t *d_out768,
+                               uint8_t *d_expect, void *stream);
+
 /* ---- notary validation of whole collations (Cfg4) ----
  * For each shard body: blob-deserialize (sharding/utils/marshal.go:144-198), RLP-decode each tx,
  * recover every sender (EIP-155 signer with chain_id), and compute the chunk root.

@@ -90,3 +90,37 @@ def test_precompile_run_semantics(ctx):
     with pytest.raises(B.ErrMalformedPoint):
         pre.Run(bytes.fromhex(bad["input"]), ctx)
     assert pre.RequiredGas(b"\x00" * 384) == 100000 + 2 * 80000
+
+
+def _synth_scalar(oracle, seed, i, tag):
+    h = oracle.keccak256(seed.to_bytes(8, "little") + i.to_bytes(8, "little") + bytes([tag, 0, 0]))
+    return int.from_bytes(h, "little") & ((1 << 253) - 1) or 1
+
+
+def test_synth_checks_match_oracle(ctx, oracle):
+    """configs[4] generator (gsv_bn256_synth_checks_dev): bytes equal the oracle's G1/G2 scalar
+    multiples of the same Keccak-derived scalars, and every check's verdict matches both the
+    oracle and the generator's expected verdict."""
+    import torch
+    n, seed = 1024, 77
+    out = torch.empty((n, 768), dtype=torch.uint8, device="cuda")
+    exp = torch.empty((n,), dtype=torch.uint8, device="cuda")
+    ctx.bn256_synth_checks_dev(seed, out, exp)
+    torch.cuda.synchronize()
+    h = out.cpu().numpy()
+    e = exp.cpu().numpy()
+    P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+    for c in [0, 1, 7, 1023]:
+        a, b, cc, d = (_synth_scalar(oracle, seed, c, t) for t in (0x61, 0x62, 0x63, 0x64))
+        d1 = d + 1 if c % 8 == 7 else d  # the false checks use -(d+1)P in the last pair
+        want = (oracle.bn256_g1_mul(a) + oracle.bn256_g2_mul(b) + oracle.bn256_g1_mul(-b % R) +
+                oracle.bn256_g2_mul(a) + oracle.bn256_g1_mul(cc) + oracle.bn256_g2_mul(d) +
+                oracle.bn256_g1_mul(-d1 % R) + oracle.bn256_g2_mul(cc))
+        if c % 1024 == 1023:
+            want = want[:384] + P.to_bytes(32, "big") + want[416:]
+        assert bytes(h[c]) == want, c
+    for c in range(0, n, 37):
+        assert e[c] == _v(oracle, bytes(h[c])), c
+    v = ctx.pairing_check_batch([bytes(r) for r in h])
+    assert (v == e).all()
+    assert (e == 1).sum() and (e == 0).sum() and (e == 2).sum() == 1
