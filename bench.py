@@ -38,6 +38,11 @@ MACS_PER_RECOVERY = 1358 * 64 + 1729 * 36 + 301 * 64
 # gfx950 v_mad_u64_u32 issue rate: half rate = 16 lanes/clk/SIMD (measured, profiles/r01_microbench_int.txt)
 PEAK_MAC = 256 * 4 * 16 * 2.4e9
 N_CHECKS = 65536           # configs[4]: 4-pair BN254 PairingCheck x 64k (split over the ranks)
+# algorithmic work per 4-pair check: F_p multiplications the reference algorithm spends (counted on
+# the oracle restatement of crypto/bn256/cloudflare, tests/test_oracle.py pins the figure), each
+# a 256-bit Montgomery product = 64 + 64 32x32-bit partial products
+FP_MULS_PER_CHECK = 106852
+MACS_PER_FP_MUL = 128
 PERMS_PER_MIB = 83016      # Keccak-f permutations per 1 MiB chunk root (data-independent)
 HBM_PEAK_GBPS = 8000.0
 
@@ -235,8 +240,14 @@ def main():
         k_prep, _ = ctx.kernel_time(_lib.K_BN_PREPARE)
         k_mill, _ = ctx.kernel_time(_lib.K_PAIRING)
         k_fin, _ = ctx.kernel_time(_lib.K_BN_FINAL)
+        k_tot = (k_prep + k_mill + k_fin) / psteps
+        p_ach = FP_MULS_PER_CHECK * MACS_PER_FP_MUL * nloc / (k_tot * 1e-3)
         pairing = {
             "checks_per_s": round(N_CHECKS * psteps / pdt, 1), "checks": N_CHECKS, "pairs_per_check": 4,
+            "roofline": {"bound": "valu", "achieved": round(p_ach / 1e12, 3), "peak": round(PEAK_MAC / 1e12, 3),
+                         "unit": "TMAC/s", "frac": round(p_ach / PEAK_MAC, 4),
+                         "algorithmic_per_unit": f"{FP_MULS_PER_CHECK} F_p Montgomery products x "
+                                                 f"{MACS_PER_FP_MUL} partial products per 4-pair check"},
             "ms_per_step": round(pdt / psteps * 1e3, 3),
             "prepare_kernel_ms": round(k_prep / psteps, 3), "miller_kernel_ms": round(k_mill / psteps, 3),
             "final_exp_kernel_ms": round(k_fin / psteps, 3),

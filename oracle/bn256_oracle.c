@@ -134,8 +134,16 @@ static void fp_sub(fp *c, const fp *a, const fp *b) { /* a + (p - b), reduce */
     }
     fp_add(c, a, &t);
 }
+/* F_p multiplication counter (algorithmic work per check, reported by bench.py) */
+static __thread uint64_t g_fp_muls;
+uint64_t oracle_bn256_fp_mul_count(int reset) {
+    uint64_t v = g_fp_muls;
+    if (reset) g_fp_muls = 0;
+    return v;
+}
 /* Montgomery product a*b*2^-256 mod p (gfpMul), CIOS form, canonical output */
 static void fp_mul(fp *c, const fp *a, const fp *b) {
+    g_fp_muls++;
     uint64_t t[6] = {0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 4; i++) {
         u128 acc;

@@ -62,4 +62,5 @@ int oracle_bn256_final_exp(const uint8_t in384[384], uint8_t out384[384]);
 int oracle_bn256_g1_mul(uint8_t out64[64], const uint8_t *in64, const uint8_t k32[32]);
 int oracle_bn256_g2_mul(uint8_t out128[128], const uint8_t *in128, const uint8_t k32[32]);
 int oracle_bn256_g2_check(const uint8_t in128[128]);
+uint64_t oracle_bn256_fp_mul_count(int reset);
 #endif

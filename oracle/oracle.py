@@ -65,6 +65,8 @@ def lib():
         L.oracle_bn256_g1_mul.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.oracle_bn256_g2_mul.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.oracle_bn256_g2_check.argtypes = [ctypes.c_char_p]
+        L.oracle_bn256_fp_mul_count.argtypes = [ctypes.c_int]
+        L.oracle_bn256_fp_mul_count.restype = ctypes.c_uint64
         _LIB = L
     return _LIB
 
@@ -220,3 +222,11 @@ def bn256_miller(pair192: bytes):
     out = ctypes.create_string_buffer(384)
     rc = lib().oracle_bn256_miller(pair192, out)
     return None if rc else out.raw
+
+
+def bn256_fp_muls(inp: bytes):
+    """F_p multiplications the reference algorithm spends on one precompile input."""
+    L = lib()
+    L.oracle_bn256_fp_mul_count(1)
+    L.oracle_bn256_pairing_check(inp, len(inp))
+    return int(L.oracle_bn256_fp_mul_count(1))

@@ -189,3 +189,10 @@ def test_bn256_subgroup_check_independent(oracle):
     # a G2 scalar multiple computed by the oracle matches pure Python
     k = 0x1234567890ABCDEF1234567890
     assert B.g2_decode(oracle.bn256_g2_mul(k)) == B.g2_mul(gen, k)
+
+
+def test_bn256_algorithmic_work_figure(oracle):
+    # bench.py FP_MULS_PER_CHECK: F_p products of the reference algorithm for one 4-pair check
+    import bench
+    g = next(x for x in golden("bn256.json")["generated"] if x["note"] == "4-pair bilinear identity (true)")
+    assert oracle.bn256_fp_muls(bytes.fromhex(g["input"])) == bench.FP_MULS_PER_CHECK
