@@ -421,7 +421,11 @@ GSV_DI void store_pub_addr(uint8_t* pub65, uint8_t* addr20, bool ok, const fe& q
 }
 
 // ---------------------------------------------------------------------------- kernels
-__global__ __launch_bounds__(256) void k_ecrecover(const uint8_t* __restrict__ msg32,
+#ifndef GSV_ECR_WAVES
+#define GSV_ECR_WAVES 2
+#endif
+// ~258 live VGPRs: 2 waves/SIMD with a couple of spilled registers beats 1 wave/SIMD spill-free
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAVES, GSV_ECR_WAVES))) void k_ecrecover(const uint8_t* __restrict__ msg32,
                                                    const uint8_t* __restrict__ sig65, uint32_t n,
                                                    const uint4* __restrict__ gtab,
                                                    uint8_t* __restrict__ pub65,

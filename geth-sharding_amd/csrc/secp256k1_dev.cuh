@@ -431,15 +431,49 @@ GSV_DI void gej_dbl(gej& r, const gej& p) {
     fe_sub(r.y, t, C);
 }
 
-// Rare path of the mixed add (p == +-q): out of line so the hot loops stay small in I-cache.
-__device__ __noinline__ void gej_add_ge_exceptional(gej* r, bool* inf, const gej* p, const fe* rr) {
-    if (fe_is_zero(*rr)) {
-        gej d;
-        gej_dbl(d, *p);
-        *r = d;
+typedef uint32_t gsv_v8 __attribute__((ext_vector_type(8)));
+typedef uint32_t gsv_v32 __attribute__((ext_vector_type(32)));
+// Rare path of the mixed add (p == q): the doubling, out of line so the hot loops stay small in
+// I-cache.  Values travel in VGPR vectors (an aggregate or a pointer argument would pin the
+// caller's accumulator to scratch memory for the whole loop).
+__device__ __noinline__ gsv_v32 gej_dbl_ool(gsv_v8 x, gsv_v8 y, gsv_v8 z) {
+    gej p, d;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        p.x.v[i] = x[i];
+        p.y.v[i] = y[i];
+        p.z.v[i] = z[i];
+    }
+    gej_dbl(d, p);
+    gsv_v32 o;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        o[i] = d.x.v[i];
+        o[8 + i] = d.y.v[i];
+        o[16 + i] = d.z.v[i];
+        o[24 + i] = 0;
+    }
+    return o;
+}
+GSV_DI void gej_add_ge_exceptional(gej& r, bool& inf, const gej& p, const fe& rr) {
+    if (fe_is_zero(rr)) {
+        gsv_v8 x, y, z;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            x[i] = p.x.v[i];
+            y[i] = p.y.v[i];
+            z[i] = p.z.v[i];
+        }
+        gsv_v32 o = gej_dbl_ool(x, y, z);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            r.x.v[i] = o[i];
+            r.y.v[i] = o[8 + i];
+            r.z.v[i] = o[16 + i];
+        }
     } else {
-        *inf = true;
-        *r = *p;
+        inf = true;
+        r = p;
     }
 }
 
@@ -455,7 +489,7 @@ GSV_DI void gej_add_ge(gej& r, bool& inf, const gej& p, const ge& q) {
     fe_sub(rr, s2, p.y);
     bool exc = fe_is_zero(h) && !inf;
     if (__builtin_expect(exc, 0)) {
-        gej_add_ge_exceptional(&r, &inf, &p, &rr);
+        gej_add_ge_exceptional(r, inf, p, rr);
         return;
     }
     fe_sqr(hh, h);

@@ -10,7 +10,8 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgsv.so")
+# GSV_LIB_PATH overrides the in-tree library (A/B timing of kernel variants only)
+LIB_PATH = os.environ.get("GSV_LIB_PATH") or os.path.join(HERE, "libgsv.so")
 
 # status codes (include/gsv.h)
 ST_OK = 0

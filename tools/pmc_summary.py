@@ -1,0 +1,87 @@
+"""Summarise a tools/profile_round.sh run (rocprofv3 SQLite outputs) into one JSON per kernel.
+
+    python tools/pmc_summary.py gpurun_out/prof/<tag> > profiles/<tag>/pmc_summary.json
+
+Per kernel: dispatches, average duration (kernel-trace pass), VGPR/scratch, HBM bytes per
+dispatch from FETCH_SIZE and WRITE_SIZE (each from its own pass), and SQ VALU counters.
+gfx950 correction (MI355X_MICROARCH.md § HBM): FETCH_SIZE counts 64 B per 128-B request for
+wide coalesced reads, so `fetch_bytes_x2` doubles it; which of the two applies depends on the
+kernel's access width — both are reported, with the raw value.
+"""
+import json
+import os
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    return name.split("(")[0]
+
+
+def counters(db, names):
+    out = defaultdict(lambda: defaultdict(list))
+    con = sqlite3.connect(db)
+    for kname, cname, val, disp, vgpr, agpr, scratch in con.execute(
+            "select kernel_name, counter_name, value, dispatch_id, vgpr_count, accum_vgpr_count, scratch_size "
+            "from counters_collection"):
+        if cname in names:
+            out[short(kname)][cname].append((disp, val))
+        out[short(kname)]["_res"] = [(0, (vgpr, agpr, scratch))]
+    return out
+
+
+def durations(db):
+    con = sqlite3.connect(db)
+    d = defaultdict(list)
+    for kname, start, end in con.execute("select name, start, end from kernels"):
+        d[short(kname)].append(end - start)
+    return d
+
+
+def per_dispatch(vals):
+    # SQ counters arrive per shader engine: sum per dispatch, then average over dispatches
+    agg = defaultdict(float)
+    for disp, v in vals:
+        agg[disp] += v
+    return sum(agg.values()) / max(len(agg), 1)
+
+
+def main(root):
+    res = {}
+    dur = durations(os.path.join(root, "trace", "run_results.db"))
+    fetch = counters(os.path.join(root, "fetch", "run_results.db"), {"FETCH_SIZE"})
+    write = counters(os.path.join(root, "write", "run_results.db"), {"WRITE_SIZE"})
+    sq = counters(os.path.join(root, "sq", "run_results.db"),
+                  {"SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+                   "GRBM_GUI_ACTIVE"})
+    for k in sorted(set(dur) | set(fetch)):
+        if k.startswith("void at::") or k.startswith("__amd"):
+            continue
+        r = {"dispatches": len(dur.get(k, [])),
+             "avg_ms": round(sum(dur[k]) / len(dur[k]) / 1e6, 4) if dur.get(k) else None}
+        if "_res" in fetch.get(k, {}):
+            vg, ag, scr = fetch[k]["_res"][0][1]
+            r.update({"vgpr": vg, "agpr": ag, "scratch_bytes_per_lane": scr})
+        if fetch.get(k, {}).get("FETCH_SIZE"):
+            kb = per_dispatch(fetch[k]["FETCH_SIZE"])
+            r["fetch_bytes_raw"] = round(kb * 1024)
+            r["fetch_bytes_x2"] = round(kb * 2048)
+        if write.get(k, {}).get("WRITE_SIZE"):
+            r["write_bytes"] = round(per_dispatch(write[k]["WRITE_SIZE"]) * 1024)
+        s = sq.get(k, {})
+        if s.get("SQ_INSTS_VALU"):
+            r["sq_insts_valu"] = per_dispatch(s["SQ_INSTS_VALU"])
+            r["sq_waves"] = per_dispatch(s["SQ_WAVES"])
+            busy = per_dispatch(s["SQ_BUSY_CYCLES"]) if s.get("SQ_BUSY_CYCLES") else None
+            act = per_dispatch(s["SQ_ACTIVE_INST_VALU"]) if s.get("SQ_ACTIVE_INST_VALU") else None
+            wcyc = per_dispatch(s["SQ_WAVE_CYCLES"]) if s.get("SQ_WAVE_CYCLES") else None
+            if act and wcyc:
+                r["valu_active_frac_of_wave_cycles"] = round(act / wcyc, 4)
+        res[k] = r
+    json.dump(res, sys.stdout, indent=1, sort_keys=True)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
