@@ -37,6 +37,9 @@ BODY = 1 << 20            # collation size limit (sharding/collation.go:45)
 MACS_PER_RECOVERY = 1358 * 64 + 1729 * 36 + 301 * 64
 # gfx950 v_mad_u64_u32 issue rate: half rate = 16 lanes/clk/SIMD (measured, profiles/r01_microbench_int.txt)
 PEAK_MAC = 256 * 4 * 16 * 2.4e9
+NOTARY_SHARDS = 100       # configs[3]: 100 shards x 8,192 txs, partitioned over the ranks
+NOTARY_TXS = 8192          # 8,192 x 128-byte blob-serialized txs = one 2^20-byte body
+NOTARY_REC = 1064          # gathered per-shard record: root 32 | ntx 4 | bitmap 1024 | pad 4
 N_CHECKS = 65536           # configs[4]: 4-pair BN254 PairingCheck x 64k (split over the ranks)
 # algorithmic work per 4-pair check: F_p multiplications the reference algorithm spends (counted on
 # the oracle restatement of crypto/bn256/cloudflare, tests/test_oracle.py pins the figure), each
@@ -129,6 +132,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-chunk-leg", action="store_true")
     ap.add_argument("--no-pairing-leg", action="store_true")
+    ap.add_argument("--no-notary-leg", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -206,11 +210,68 @@ def main():
             "bottom_kernel_avg_ms": round(leaf_ms / max(leaf_n, 1), 4),
             "level_kernels_ms_per_step": round(lvl_ms / csteps, 4),
         }
-        # parity spot check of one shard against the oracle (outside the timed region)
-        if rank == 0:
-            from oracle import oracle as O
-            b0 = bodies[:BODY].cpu().numpy()
-            assert bytes(roots[0].cpu().numpy()) == O.derive_sha_bytes(b0), "chunk root mismatch vs oracle"
+
+    # ---------------------------------------------------------------- notary leg (configs[3])
+    # shard-ID partition: rank r owns shards [100r/G, 100(r+1)/G); blob decode + tx RLP + Sender
+    # recovery + chunk root on the GPU, then one RCCL all-gather of fixed-size per-shard records
+    notary = None
+    if not args.no_notary_leg:
+        from gsv import shards as SH
+        lo, hi = SH.shard_range(rank, ws, NOTARY_SHARDS)
+        nloc = hi - lo
+        per_rank = SH.shards_per_rank(ws, NOTARY_SHARDS)
+        rbytes = SH.record_bytes(NOTARY_TXS)
+        nb = torch.empty((nloc * NOTARY_TXS * 128,), dtype=torch.uint8, device=dev)
+        n_exp = torch.empty((nloc * NOTARY_TXS,), dtype=torch.uint8, device=dev)
+        ctx.notary_synth_dev(777, lo, nloc, NOTARY_TXS, nb, n_exp, None, stream=stream)
+        n_off = np.arange(nloc + 1, dtype=np.uint64) * NOTARY_TXS * 128
+        n_root = torch.empty((nloc, 32), dtype=torch.uint8, device=dev)
+        n_cnt = torch.empty((nloc,), dtype=torch.int32, device=dev)
+        n_bm = torch.empty((nloc, NOTARY_TXS // 8), dtype=torch.uint8, device=dev)
+        n_st = torch.empty((nloc, NOTARY_TXS), dtype=torch.uint8, device=dev)
+        rec = torch.zeros((per_rank, rbytes), dtype=torch.uint8, device=dev)
+        gathered = torch.zeros((ws * per_rank, rbytes), dtype=torch.uint8, device=dev)
+
+        def notary_step(with_status=False):
+            ctx.notary_validate_shards_dev(nb, n_off, n_root, n_cnt, n_bm, None, n_st if with_status else None,
+                                           max_txs=NOTARY_TXS, stream=stream)
+            with torch.cuda.stream(stream):
+                SH.pack_records(rec, n_root, n_cnt, n_bm)
+                SH.gather_records(rec, ws, gathered)
+
+        notary_step(with_status=True)
+        stream.synchronize()
+        # full-size parity property: every tx status equals the generator's construction
+        assert torch.equal(n_st.view(-1), n_exp), "notary statuses differ from the constructed truth"
+        nsteps = max(2, args.steps // 2)
+        ctx.reset_timing()
+        ctx.set_timing(True)
+        barrier(ws)
+        t4 = time.perf_counter()
+        for _ in range(nsteps):
+            notary_step()
+        stream.synchronize()
+        barrier(ws)
+        ndt = max_over_ranks(time.perf_counter() - t4, ws)
+        ctx.set_timing(False)
+        k_not, _ = ctx.kernel_time(_lib.K_NOTARY)
+        # gathered records on every rank: 100 shards of 8,192 txs each and the construction's
+        # validity bitmap (tx j invalid iff j % 128 == 127)
+        g_root, g_ntx, g_bm = SH.unpack_records(gathered, ws, NOTARY_SHARDS, NOTARY_TXS)
+        assert g_root.shape[0] == NOTARY_SHARDS and bool((g_ntx == NOTARY_TXS).all())
+        want_bm = torch.full((NOTARY_TXS // 8,), 0xFF, dtype=torch.uint8, device=dev)
+        want_bm[15::16] = 0x7F
+        assert bool((g_bm == want_bm).all()), "gathered validity bitmaps wrong"
+        notary = {
+            "shards_per_s": round(NOTARY_SHARDS * nsteps / ndt, 2),
+            "txs_per_s": round(NOTARY_SHARDS * NOTARY_TXS * nsteps / ndt, 1),
+            "shards": NOTARY_SHARDS, "txs_per_shard": NOTARY_TXS, "shards_per_rank": per_rank,
+            "ms_per_step": round(ndt / nsteps * 1e3, 3),
+            "tx_kernels_ms_per_step": round(k_not / nsteps, 3),
+            "collective": "all_gather_into_tensor (RCCL)" if ws > 1 else "none (1 rank)",
+            "gathered_bytes_per_step": ws * per_rank * rbytes,
+            "scaling": "strong",
+        }
 
     # ---------------------------------------------------------------- pairing leg (configs[4])
     pairing = None
@@ -269,8 +330,23 @@ def main():
                          f"{'libsecp256k1 secp256k1_ext_ecdsa_recover (oracle/_ref)' if kind == 'reference' else 'oracle restatement'}"
                          f", {threads} threads"}
         if chunk is not None:
+            from oracle import oracle as O
             cbody = bodies[:BODY].cpu().numpy().tobytes()
             chunk["cpu_collation_GBps_1core_oracle"] = round(cpu_baseline_chunk_root(cbody, 1), 4)
+            assert bytes(roots[0].cpu().numpy()) == O.derive_sha_bytes(cbody), "chunk root mismatch vs oracle"
+        if notary is not None:
+            from oracle import oracle as O
+            body0 = nb[:NOTARY_TXS * 128].cpu().numpy().tobytes()
+            t5 = time.perf_counter()
+            blobs = O.blob_deserialize(body0)
+            samp = [O.tx_sender(b, 1, 0) for b, _ in blobs[:512]]
+            t_tx = (time.perf_counter() - t5) / 512
+            t6 = time.perf_counter()
+            root0 = O.derive_sha_bytes(body0)
+            t_root = time.perf_counter() - t6
+            notary["cpu_shards_per_s_1core_oracle"] = round(1.0 / (t_tx * NOTARY_TXS + t_root), 4)
+            assert root0 == bytes(n_root[0].cpu().numpy()), "notary chunk root mismatch vs oracle"
+            assert [st for st, _ in samp] == n_exp[:512].cpu().tolist(), "notary statuses vs oracle"
         if pairing is not None:
             from oracle import oracle as O
             hin = pin[:64].cpu().numpy()
@@ -308,6 +384,8 @@ def main():
             line["chunk_root"] = chunk
         if pairing is not None:
             line["bn256_pairing"] = pairing
+        if notary is not None:
+            line["notary"] = notary
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist

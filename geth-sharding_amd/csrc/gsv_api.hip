@@ -38,6 +38,8 @@ struct gsv_ctx {
     std::vector<hipEvent_t> open_ev;  // timer events opened by launch hooks
     hipStream_t cur_stream = nullptr;
     std::mutex wmu;                   // serializes users of `work`
+    uint8_t* nwork = nullptr;         // notary workspace (blob tables, chain-id buffers)
+    size_t nwork_cap = 0;
 };
 
 namespace {
@@ -226,6 +228,7 @@ void gsv_ctx_destroy(gsv_ctx* c) {
     for (auto e : c->free_events) hipEventDestroy(e);
     if (c->arena) hipFree(c->arena);
     if (c->work) hipFree(c->work);
+    if (c->nwork) hipFree(c->nwork);
     if (c->gtab) hipFree(c->gtab);
     hipStreamDestroy(c->stream);
     delete c;
@@ -696,49 +699,141 @@ int gsv_bn256_synth_checks_dev(gsv_ctx* c, uint64_t seed, size_t nchecks, uint8_
                                            stream ? (hipStream_t)stream : c->stream));
 }
 
-// ------------------------------------------------------------------ notary validation (Cfg4)
-int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n_shards,
-                               const uint8_t* chain_id, size_t chain_id_len, uint32_t max_txs,
-                               uint8_t* root32_out, uint32_t* ntx_out, uint8_t* valid_bitmap_out,
-                               uint8_t* senders_out) {
-    if (!c || (n_shards && (!bodies || !off || !root32_out || !ntx_out || !valid_bitmap_out))) return GSV_E_INVALID_ARG;
-    if (chain_id_len && !chain_id) return GSV_E_INVALID_ARG;
-    if (n_shards == 0) return GSV_SUCCESS;
-    // 1. chunk roots (GPU)
-    int rc = gsv_chunk_root_batch(c, bodies, off, n_shards, root32_out);
-    if (rc) return rc;
-    // 2. blob-deserialize each body into tx RLPs (sharding/collation.go:193-206)
-    std::vector<uint8_t> txdata;
-    std::vector<uint64_t> boff;
-    std::vector<size_t> first(n_shards + 1);
-    for (size_t s = 0; s < n_shards; s++) {
-        first[s] = boff.size() / 2;
-        gsv::blob_deserialize(bodies + off[s], off[s + 1] - off[s], txdata, boff);
+// ------------------------------------------------------------------ notary validation (configs[3])
+int gsv_notary_synth_dev(gsv_ctx* c, uint64_t seed, uint32_t shard0, size_t n_shards, uint32_t txs_per_shard,
+                         uint8_t* d_bodies, uint8_t* d_exp_status, uint8_t* d_exp_sender, void* stream) {
+    if (!c || (n_shards && !d_bodies) || (uint64_t)n_shards * txs_per_shard > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    return hip_err(gsv::launch_notary_synth(seed, shard0, (uint32_t)n_shards, txs_per_shard, c->gtab, d_bodies,
+                                            d_exp_status, d_exp_sender, stream ? (hipStream_t)stream : c->stream));
+}
+
+static int notary_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* start, const uint64_t* end,
+                           size_t n, const uint8_t* cid, size_t cidlen, int signer_kind, uint32_t max_txs,
+                           uint8_t* d_root, uint32_t* d_ntx, uint8_t* d_bitmap, uint8_t* d_senders, uint8_t* d_status,
+                           hipStream_t st) {
+    if (cidlen > 64) return GSV_E_INVALID_ARG;
+    for (size_t i = 0; i < n; i++)
+        if (end[i] < start[i] || end[i] - start[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+    // chain-id buffers: 64-byte big-endian value and the sighash suffix rlp(chainId) || 0x80 0x80
+    uint8_t host[256] = {0};
+    memcpy(host + 64 - cidlen, cid, cidlen);
+    size_t z = 0;
+    while (z < cidlen && cid[z] == 0) z++;
+    size_t cn = cidlen - z, sl = 0;
+    uint8_t* suf = host + 64;
+    if (cn == 1 && cid[z] < 0x80) suf[sl++] = cid[z];
+    else {
+        suf[sl++] = (uint8_t)(0x80 + cn);
+        memcpy(suf + sl, cid + z, cn);
+        sl += cn;
     }
-    first[n_shards] = boff.size() / 2;
-    size_t ntx = first[n_shards];
-    std::vector<uint64_t> toff(ntx + 1, 0);
-    for (size_t t = 0; t < ntx; t++) toff[t] = boff[2 * t];
-    if (ntx) toff[ntx] = boff[2 * ntx - 1];
-    // blobs are contiguous in txdata (each blob's end == next blob's start)
-    std::vector<uint8_t> addr(ntx * 20), st(ntx);
-    if (ntx) {
-        std::lock_guard<std::mutex> g(c->mu);
-        HIPCHK(hipSetDevice(c->device));
-        txdata.push_back(0);
-        rc = tx_sender_impl(c, txdata.data(), toff.data(), ntx, chain_id, chain_id_len, GSV_SIGNER_EIP155,
-                            addr.data(), st.data());
+    suf[sl++] = 0x80;
+    suf[sl++] = 0x80;
+    std::vector<uint64_t> offs(n);
+    std::vector<uint32_t> lens(n);
+    for (size_t i = 0; i < n; i++) {
+        offs[i] = start[i];
+        lens[i] = (uint32_t)(end[i] - start[i]);
+    }
+    size_t bm = (max_txs + 7) / 8;
+    size_t need = al(256) + al(n * 8) + al(n * 4) + al(n * 4) + al((size_t)n * max_txs * gsv::blob_rec_bytes());
+    if (need > c->nwork_cap) {
+        size_t cap = std::max(need, (size_t)16 << 20);
+        if (c->nwork) {
+            hipDeviceSynchronize();
+            hipFree(c->nwork);
+            c->nwork = nullptr;
+            c->nwork_cap = 0;
+        }
+        if (hipMalloc(&c->nwork, cap) != hipSuccess) return GSV_E_NOMEM;
+        c->nwork_cap = cap;
+    }
+    Carve cv(c->nwork);
+    uint8_t* d_cid = cv.take<uint8_t>(256);
+    uint64_t* d_off = cv.take<uint64_t>(n * 8);
+    uint32_t* d_len = cv.take<uint32_t>(n * 4);
+    uint32_t* d_cnt = d_ntx ? d_ntx : cv.take<uint32_t>(n * 4);
+    void* d_blobs = cv.take<uint8_t>((size_t)n * max_txs * gsv::blob_rec_bytes());
+    HIPCHK(hipMemcpyAsync(d_cid, host, 256, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_off, offs.data(), n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_len, lens.data(), n * 4, hipMemcpyHostToDevice, st));
+    if (d_senders) HIPCHK(hipMemsetAsync(d_senders, 0, (size_t)n * max_txs * 20, st));
+    if (d_status) HIPCHK(hipMemsetAsync(d_status, GSV_ST_BAD_RLP, (size_t)n * max_txs, st));
+    c->cur_stream = st;
+    hook_begin(c, GSV_K_NOTARY);
+    HIPCHK(gsv::launch_blob_index(d_bodies, d_off, d_len, (uint32_t)n, max_txs, d_blobs, d_cnt, st));
+    HIPCHK(gsv::launch_notary_tx(d_bodies, d_off, d_blobs, d_cnt, (uint32_t)n, max_txs, d_cid, d_cid + 64,
+                                 (uint32_t)sl, signer_kind, c->gtab, d_bitmap, (uint32_t)bm, d_senders, d_status,
+                                 st));
+    hook_end(c, GSV_K_NOTARY);
+    // chunk roots of the same bodies (own workspace)
+    return chunk_root_dev_impl(c, d_bodies, start, end, n, d_root, st);
+}
+
+int gsv_notary_validate_shards_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n_shards,
+                                   const uint8_t* chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
+                                   uint8_t* d_root32, uint32_t* d_ntx, uint8_t* d_bitmap, uint8_t* d_senders,
+                                   uint8_t* d_status, void* stream) {
+    if (!c || (n_shards && (!d_bodies || !h_off || !d_root32 || !d_bitmap))) return GSV_E_INVALID_ARG;
+    if ((chain_id_len && !chain_id) || signer_kind < GSV_SIGNER_EIP155 || signer_kind > GSV_SIGNER_FRONTIER)
+        return GSV_E_INVALID_ARG;
+    if (n_shards == 0) return GSV_SUCCESS;
+    if (n_shards > 65535 || max_txs == 0) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->wmu);
+    HIPCHK(hipSetDevice(c->device));
+    return notary_dev_impl(c, d_bodies, h_off, h_off + 1, n_shards, chain_id, chain_id_len, signer_kind, max_txs,
+                           d_root32, d_ntx, d_bitmap, d_senders, d_status, stream ? (hipStream_t)stream : c->stream);
+}
+
+int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n_shards,
+                               const uint8_t* chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
+                               uint8_t* root32_out, uint32_t* ntx_out, uint8_t* valid_bitmap_out,
+                               uint8_t* senders_out, uint8_t* status_out) {
+    if (!c || (n_shards && (!bodies || !off || !root32_out || !ntx_out || !valid_bitmap_out))) return GSV_E_INVALID_ARG;
+    if ((chain_id_len && !chain_id) || signer_kind < GSV_SIGNER_EIP155 || signer_kind > GSV_SIGNER_FRONTIER)
+        return GSV_E_INVALID_ARG;
+    if (n_shards == 0) return GSV_SUCCESS;
+    if (n_shards > 65535 || max_txs == 0 || chain_id_len > 64) return GSV_E_INVALID_ARG;
+    for (size_t i = 0; i < n_shards; i++)
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint64_t> st(n_shards), en(n_shards);
+    uint64_t pos = 0;
+    for (size_t i = 0; i < n_shards; i++) {
+        st[i] = pos;
+        en[i] = pos + (off[i + 1] - off[i]);
+        pos = (en[i] + 15) & ~15ull;
+    }
+    size_t bm = (max_txs + 7) / 8, nt = n_shards * (size_t)max_txs;
+    int rc = arena_reserve(c, al(pos + 16) + al(n_shards * 32) + al(n_shards * 4) + al(n_shards * bm) +
+                                  al(nt * 20) + al(nt));
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_b = cv.take<uint8_t>(pos + 16);
+    uint8_t* d_r = cv.take<uint8_t>(n_shards * 32);
+    uint32_t* d_n = cv.take<uint32_t>(n_shards * 4);
+    uint8_t* d_bm = cv.take<uint8_t>(n_shards * bm);
+    uint8_t* d_snd = senders_out ? cv.take<uint8_t>(nt * 20) : nullptr;
+    uint8_t* d_st = status_out ? cv.take<uint8_t>(nt) : nullptr;
+    for (size_t i = 0; i < n_shards; i++)
+        if (en[i] > st[i])
+            HIPCHK(hipMemcpyAsync(d_b + st[i], bodies + off[i], en[i] - st[i], hipMemcpyHostToDevice, c->stream));
+    {
+        std::lock_guard<std::mutex> g2(c->wmu);
+        rc = notary_dev_impl(c, d_b, st.data(), en.data(), n_shards, chain_id, chain_id_len, signer_kind, max_txs,
+                             d_r, d_n, d_bm, d_snd, d_st, c->stream);
         if (rc) return rc;
     }
-    size_t bm_bytes = (max_txs + 7) / 8;
-    memset(valid_bitmap_out, 0, bm_bytes * n_shards);
-    for (size_t s = 0; s < n_shards; s++) {
-        size_t cnt = first[s + 1] - first[s];
-        ntx_out[s] = (uint32_t)cnt;
-        for (size_t t = 0; t < cnt && t < max_txs; t++)
-            if (st[first[s] + t] == GSV_ST_OK) valid_bitmap_out[s * bm_bytes + t / 8] |= (uint8_t)(1u << (t % 8));
-    }
-    if (senders_out && ntx) memcpy(senders_out, addr.data(), ntx * 20);
+    HIPCHK(hipMemcpyAsync(root32_out, d_r, n_shards * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(ntx_out, d_n, n_shards * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(valid_bitmap_out, d_bm, n_shards * bm, hipMemcpyDeviceToHost, c->stream));
+    if (senders_out) HIPCHK(hipMemcpyAsync(senders_out, d_snd, nt * 20, hipMemcpyDeviceToHost, c->stream));
+    if (status_out) HIPCHK(hipMemcpyAsync(status_out, d_st, nt, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < n_shards; i++)
+        if (ntx_out[i] > max_txs) return GSV_E_TOO_LARGE;
     return GSV_SUCCESS;
 }
 

@@ -38,6 +38,19 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
 
 hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st);
 
+// notary.hip
+size_t blob_rec_bytes();
+hipError_t launch_blob_index(const uint8_t* d_bodies, const uint64_t* d_off, const uint32_t* d_len,
+                             uint32_t n_shards, uint32_t max_txs, void* d_blobs, uint32_t* d_ntx, hipStream_t st);
+hipError_t launch_notary_tx(const uint8_t* d_bodies, const uint64_t* d_off, const void* d_blobs,
+                            const uint32_t* d_ntx, uint32_t n_shards, uint32_t max_txs, const uint8_t* d_cid64,
+                            const uint8_t* d_suffix, uint32_t slen, int signer_kind, const uint4* gtab,
+                            uint8_t* d_bitmap, uint32_t bm_bytes, uint8_t* d_senders, uint8_t* d_status,
+                            hipStream_t st);
+hipError_t launch_notary_synth(uint64_t seed, uint32_t shard0, uint32_t n_shards, uint32_t txs_per_shard,
+                               const uint4* gtab, uint8_t* d_bodies, uint8_t* d_exp_status, uint8_t* d_exp_sender,
+                               hipStream_t st);
+
 constexpr size_t GTAB_ENTRIES = 32 * 256;
 constexpr size_t GTAB_BYTES = GTAB_ENTRIES * 64;
 

@@ -1,0 +1,476 @@
+// secp256k1 public-key recovery core shared by the ecrecover, sender and notary kernels.
+// See ecrecover.hip for the algorithm and the reference semantics it restates.
+#pragma once
+#include "gsv_internal.h"
+#include "keccak_dev.cuh"
+#include "secp256k1_dev.cuh"
+
+namespace gsv {
+
+__device__ constexpr uint32_t BETA[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
+                                         0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+__device__ constexpr uint32_t MINUS_LAMBDA[8] = {0xB51283CFu, 0xE0CFC810u, 0x8EC739C2u, 0xA880B9FCu,
+                                                 0x77ED9BA4u, 0x5AD9E3FDu, 0x3FA3CF1Fu, 0xAC9C52B3u};
+__device__ constexpr uint32_t MINUS_B1[8] = {0x0ABFE4C3u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u,
+                                             0u, 0u, 0u, 0u};
+__device__ constexpr uint32_t MINUS_B2[8] = {0x3DB1562Cu, 0xD765CDA8u, 0x0774346Du, 0x8A280AC5u,
+                                             0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+__device__ constexpr uint32_t GLV_G1[8] = {0xEB153DABu, 0x90E49284u, 0x6BCDE86Cu, 0xD221A7D4u,
+                                           0x00003086u, 0u, 0u, 0u};
+__device__ constexpr uint32_t GLV_G2[8] = {0xE4C42212u, 0x7FA90ABFu, 0x88286F54u, 0x7ED6010Eu,
+                                           0x0000E443u, 0u, 0u, 0u};
+__device__ constexpr uint32_t GX[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
+                                       0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
+__device__ constexpr uint32_t GY[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                                       0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+__device__ constexpr uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC4u, 0x45512319u,
+                                              0x00000001u, 0u, 0u, 0u};
+__device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
+                                           0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
+
+constexpr int GLV_DIGITS = 44;  // w = 3 odd digits cover k < 2^131 (bound is 2^128)
+
+// ---------------------------------------------------------------------------- scalar helpers
+GSV_DI void sc_from_const(sc& r, const uint32_t c[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = c[i];
+}
+
+// (k * g) >> 272, rounded (libsecp256k1 scalar_8x32_impl.h mul_shift_var semantics)
+GSV_DI void sc_mul_shift272(sc& r, const sc& k, const uint32_t g[8]) {
+    uint32_t t[16];
+    mul_8x8_asm(t, k.v, g);
+#pragma unroll
+    for (int i = 0; i < 7; i++) r.v[i] = (t[8 + i] >> 16) | (t[9 + i] << 16);
+    r.v[7] = t[15] >> 16;
+    uint64_t c = (uint64_t)r.v[0] + ((t[8] >> 15) & 1u);
+    r.v[0] = lo32(c);
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+        c = (uint64_t)r.v[i] + hi32(c);
+        r.v[i] = lo32(c);
+    }
+}
+
+// k = r1 + r2 * lambda (mod n)  (libsecp256k1 scalar_impl.h secp256k1_scalar_split_lambda)
+GSV_DI void sc_split_lambda(sc& r1, sc& r2, const sc& k) {
+    sc c1, c2, t;
+    sc_mul_shift272(c1, k, GLV_G1);
+    sc_mul_shift272(c2, k, GLV_G2);
+    sc_from_const(t, MINUS_B1);
+    sc_mul(c1, c1, t);
+    sc_from_const(t, MINUS_B2);
+    sc_mul(c2, c2, t);
+    sc_add(r2, c1, c2);
+    sc_from_const(t, MINUS_LAMBDA);
+    sc_mul(r1, r2, t);
+    sc_add(r1, r1, k);
+}
+
+GSV_DI bool sc_is_high(const sc& a) { return limbs_lt(HALF_N, a.v); }
+
+// Fixed-schedule odd-digit recoding, w = 3: k (odd after skew) = sum d_i 8^i with
+// d_i in {+-1,+-3,+-5,+-7}.  Digit i packed in 4 bits: bit 3 = negative, bits 0-1 = (|d|-1)/2.
+GSV_DI void recode_w3(uint32_t dig[6], uint32_t& skew, const sc& kin) {
+    uint32_t k[5] = {kin.v[0], kin.v[1], kin.v[2], kin.v[3], kin.v[4]};
+    skew = (k[0] & 1u) ^ 1u;
+    // k += skew  (k < 2^129 so no overflow out of 5 limbs)
+    uint64_t c = (uint64_t)k[0] + skew;
+    k[0] = lo32(c);
+#pragma unroll
+    for (int i = 1; i < 5; i++) {
+        c = (uint64_t)k[i] + hi32(c);
+        k[i] = lo32(c);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) dig[i] = 0;
+#pragma unroll
+    for (int i = 0; i < GLV_DIGITS; i++) {
+        int32_t d;
+        if (i < GLV_DIGITS - 1) d = (int32_t)(k[0] & 15u) - 8;
+        else d = (int32_t)(k[0] & 15u);
+        uint32_t neg = d < 0 ? 1u : 0u;
+        uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+        uint32_t code = (neg << 3) | ((mag - 1u) >> 1);
+        dig[i >> 3] |= code << ((i & 7) * 4);
+        // k = (k - d) >> 3
+        int64_t t = (int64_t)k[0] - d;
+        uint32_t kk[5];
+        kk[0] = (uint32_t)t;
+        int64_t carry = t >> 32;
+#pragma unroll
+        for (int j = 1; j < 5; j++) {
+            int64_t u = (int64_t)k[j] + carry;
+            kk[j] = (uint32_t)u;
+            carry = u >> 32;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) k[j] = (kk[j] >> 3) | (kk[j + 1] << 29);
+        k[4] = kk[4] >> 3;
+    }
+}
+
+// ---------------------------------------------------------------------------- group helpers
+GSV_DI void ge_cmov(ge& r, const ge& a, bool f) {
+    fe_cmov(r.x, a.x, f);
+    fe_cmov(r.y, a.y, f);
+}
+
+// mixed add with the z-ratio output (no exceptional cases possible where it is used)
+GSV_DI void gej_add_ge_zr(gej& r, fe& zr, const gej& p, const ge& q) {
+    fe z1z1, u2, s2, h, hh, i4, j, rr, v, t;
+    fe_sqr(z1z1, p.z);
+    fe_mul(u2, q.x, z1z1);
+    fe_mul(s2, q.y, p.z);
+    fe_mul(s2, s2, z1z1);
+    fe_sub(h, u2, p.x);
+    fe_sub(rr, s2, p.y);
+    fe_sqr(hh, h);
+    fe_add(i4, hh, hh);
+    fe_add(i4, i4, i4);
+    fe_mul(j, h, i4);
+    fe_add(rr, rr, rr);
+    fe_mul(v, p.x, i4);
+    gej o;
+    fe_sqr(t, rr);
+    fe_sub(t, t, j);
+    fe_sub(t, t, v);
+    fe_sub(o.x, t, v);
+    fe_sub(t, v, o.x);
+    fe_mul(t, rr, t);
+    fe_mul(v, p.y, j);
+    fe_add(v, v, v);
+    fe_sub(o.y, t, v);
+    fe_add(t, p.z, h);
+    fe_sqr(t, t);
+    fe_sub(t, t, z1z1);
+    fe_sub(o.z, t, hh);
+    fe_add(zr, h, h);  // Z3 = 2 * Z1 * H
+    r = o;
+}
+
+// (X, Y) scaled to Z * f: (X f^2, Y f^3)
+GSV_DI void scale_xy(ge& r, const fe& x, const fe& y, const fe& f) {
+    fe f2, f3;
+    fe_sqr(f2, f);
+    fe_mul(f3, f2, f);
+    fe_mul(r.x, x, f2);
+    fe_mul(r.y, y, f3);
+}
+
+// Odd multiples {1,3,5,7}R as affine points of an isomorphic curve E'' (no inversion);
+// a Jacobian result (X,Y,Z) on E'' is (X, Y, Z * zfac) on E.
+GSV_DI void build_r_table(ge T[4], fe& zfac, const fe& x, const fe& y) {
+    gej R1;
+    R1.x = x;
+    R1.y = y;
+    fe_set_u32(R1.z, 1);
+    gej D;
+    gej_dbl(D, R1);
+    fe u2, u3;
+    fe_sqr(u2, D.z);
+    fe_mul(u3, u2, D.z);
+    ge Dp;
+    Dp.x = D.x;
+    Dp.y = D.y;
+    gej P1, P3, P5, P7;
+    fe_mul(P1.x, x, u2);
+    fe_mul(P1.y, y, u3);
+    fe_set_u32(P1.z, 1);
+    fe zr3, zr5, zr7;
+    gej_add_ge_zr(P3, zr3, P1, Dp);
+    gej_add_ge_zr(P5, zr5, P3, Dp);
+    gej_add_ge_zr(P7, zr7, P5, Dp);
+    T[3].x = P7.x;
+    T[3].y = P7.y;
+    scale_xy(T[2], P5.x, P5.y, zr7);
+    fe f;
+    fe_mul(f, zr5, zr7);
+    scale_xy(T[1], P3.x, P3.y, f);
+    fe_mul(f, f, zr3);
+    scale_xy(T[0], P1.x, P1.y, f);
+    fe_mul(zfac, D.z, P7.z);
+}
+
+GSV_DI void table_select(ge& out, const ge T[4], uint32_t idx) {
+    out = T[0];
+#pragma unroll
+    for (int e = 1; e < 4; e++) ge_cmov(out, T[e], idx == (uint32_t)e);
+}
+GSV_DI void table_select_x(fe& out, const fe X[4], uint32_t idx) {
+    out = X[0];
+#pragma unroll
+    for (int e = 1; e < 4; e++) fe_cmov(out, X[e], idx == (uint32_t)e);
+}
+
+// u*G with the byte-window comb table (gtab[w*256 + d] = d * 2^(8w) * G, affine, 16 words)
+GSV_DI void comb_mul_g(gej& acc, bool& inf, const sc& u, const uint4* __restrict__ gtab) {
+    inf = true;
+    const uint4* e = gtab + (size_t)(u.v[0] & 0xFFu) * 4;
+    uint4 n0 = e[0], n1 = e[1], n2 = e[2], n3 = e[3];
+#pragma unroll 1
+    for (int w = 0; w < 32; w++) {
+        uint32_t d = (sel_word(u.v, (uint32_t)w >> 2) >> ((w & 3) * 8)) & 0xFFu;
+        ge P;
+        P.x.v[0] = n0.x; P.x.v[1] = n0.y; P.x.v[2] = n0.z; P.x.v[3] = n0.w;
+        P.x.v[4] = n1.x; P.x.v[5] = n1.y; P.x.v[6] = n1.z; P.x.v[7] = n1.w;
+        P.y.v[0] = n2.x; P.y.v[1] = n2.y; P.y.v[2] = n2.z; P.y.v[3] = n2.w;
+        P.y.v[4] = n3.x; P.y.v[5] = n3.y; P.y.v[6] = n3.z; P.y.v[7] = n3.w;
+        if (w < 31) {  // prefetch next window's entry
+            uint32_t dn = (sel_word(u.v, (uint32_t)(w + 1) >> 2) >> (((w + 1) & 3) * 8)) & 0xFFu;
+            const uint4* en = gtab + ((size_t)(w + 1) * 256 + dn) * 4;
+            n0 = en[0]; n1 = en[1]; n2 = en[2]; n3 = en[3];
+        }
+        gej t;
+        bool tinf = inf;
+        gej_add_ge(t, tinf, acc, P);
+        if (d != 0) {
+            acc = t;
+            inf = tinf;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------- recovery core
+// Returns GSV_ST_OK or GSV_ST_RECOVER_FAILED; on OK (qx, qy) is the affine public key.
+// msg/r/s are 256-bit values as little-endian limbs; recid in 0..3.
+GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32_t r[8],
+                             const uint32_t s[8], uint32_t recid, const uint4* __restrict__ gtab) {
+    bool ok = limbs_lt(r, SN) && limbs_lt(s, SN);
+    sc rs, ss, m;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        rs.v[i] = r[i];
+        ss.v[i] = s[i];
+    }
+    ok = ok && !sc_is_zero(rs) && !sc_is_zero(ss);
+    sc_cond_sub_n(m.v, msg, 0);  // msg mod n (msg < 2^256 < 2n)
+
+    // x = r (+ n when recid & 2; fails for r >= p - n)
+    fe x;
+    {
+        bool hi = (recid & 2u) != 0;
+        ok = ok && (!hi || limbs_lt(r, P_MINUS_N));
+        uint64_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            c = (uint64_t)r[i] + (hi ? SN[i] : 0u) + hi32(c);
+            x.v[i] = lo32(c);
+        }
+    }
+    // y = sqrt(x^3 + 7), parity recid & 1
+    fe y, t;
+    fe_sqr(t, x);
+    fe_mul(t, t, x);
+    fe seven;
+    fe_set_u32(seven, 7);
+    fe_add(t, t, seven);
+    ok = ok && fe_sqrt(y, t);
+    {
+        fe ny;
+        fe_neg(ny, y);
+        fe_cmov(y, ny, (y.v[0] & 1u) != (recid & 1u));
+    }
+    // u1 = -m / r, u2 = s / r
+    sc rn, u1, u2;
+    sc_inv(rn, rs);
+    sc_mul(u1, rn, m);
+    sc_neg(u1, u1);
+    sc_mul(u2, rn, ss);
+
+    // ---- u2 * R via GLV + fixed w=3 odd digits
+    sc k1, k2;
+    sc_split_lambda(k1, k2, u2);
+    bool neg1 = sc_is_high(k1), neg2 = sc_is_high(k2);
+    {
+        sc nk;
+        sc_neg(nk, k1);
+#pragma unroll
+        for (int i = 0; i < 8; i++) k1.v[i] = neg1 ? nk.v[i] : k1.v[i];
+        sc_neg(nk, k2);
+#pragma unroll
+        for (int i = 0; i < 8; i++) k2.v[i] = neg2 ? nk.v[i] : k2.v[i];
+    }
+    uint32_t dig1[6], dig2[6], skew1, skew2;
+    recode_w3(dig1, skew1, k1);
+    recode_w3(dig2, skew2, k2);
+
+    ge T[4];
+    fe zfac;
+    build_r_table(T, zfac, x, y);
+    fe LX[4];
+    {
+        fe beta;
+#pragma unroll
+        for (int i = 0; i < 8; i++) beta.v[i] = BETA[i];
+#pragma unroll
+        for (int e = 0; e < 4; e++) fe_mul(LX[e], T[e].x, beta);
+    }
+
+    gej acc;
+    bool ainf = true;
+    acc.x = T[0].x;
+    acc.y = T[0].y;
+    fe_set_u32(acc.z, 1);
+#pragma unroll 1
+    for (int i = GLV_DIGITS - 1; i >= 0; i--) {
+        if (i != GLV_DIGITS - 1) {
+#pragma unroll 1
+            for (int d = 0; d < 3; d++) gej_dbl(acc, acc);
+        }
+        uint32_t c1 = (sel_word(dig1, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
+        uint32_t c2 = (sel_word(dig2, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
+        // one add body, two passes: digit of k1 on T, digit of k2 on lambda(T)
+#pragma unroll 1
+        for (int j = 0; j < 2; j++) {
+            uint32_t c = j ? c2 : c1;
+            bool ng = j ? neg2 : neg1;
+            ge P;
+            table_select(P, T, c & 3u);
+            fe lx;
+            table_select_x(lx, LX, c & 3u);
+            fe_cmov(P.x, lx, j != 0);
+            fe ny;
+            fe_neg(ny, P.y);
+            fe_cmov(P.y, ny, ((c >> 3) != 0) != ng);
+            gej_add_ge(acc, ainf, acc, P);
+        }
+    }
+    // skew corrections: the recoded scalars were k + skew -> subtract (+-)T0 / (+-)lambda(T0)
+#pragma unroll 1
+    for (int j = 0; j < 2; j++) {
+        bool ng = j ? neg2 : neg1;
+        uint32_t sk = j ? skew2 : skew1;
+        ge P;
+        P.x = T[0].x;
+        fe_cmov(P.x, LX[0], j != 0);
+        fe_neg(P.y, T[0].y);
+        fe_cmov(P.y, T[0].y, ng);
+        gej tmp;
+        bool tinf = ainf;
+        gej_add_ge(tmp, tinf, acc, P);
+        if (sk) {
+            acc = tmp;
+            ainf = tinf;
+        }
+    }
+    fe_mul(acc.z, acc.z, zfac);  // back from E'' to E
+
+    // ---- u1 * G via comb
+    gej accg;
+    bool ginf;
+    comb_mul_g(accg, ginf, u1, gtab);
+
+    // ---- Q = u2 R + u1 G
+    gej q;
+    bool qinf;
+    gej_add(q, qinf, acc, ainf, accg, ginf);
+    ok = ok && !qinf;
+
+    fe zi, zi2;
+    fe_inv(zi, q.z);
+    fe_sqr(zi2, zi);
+    fe_mul(qx, q.x, zi2);
+    fe_mul(zi2, zi2, zi);
+    fe_mul(qy, q.y, zi2);
+    return ok ? GSV_ST_OK : GSV_ST_RECOVER_FAILED;
+}
+
+GSV_DI void load32_be(uint32_t v[8], const uint8_t* p) { limbs_from_be(v, p); }
+
+GSV_DI void store_pub_addr(uint8_t* pub65, uint8_t* addr20, bool ok, const fe& qx, const fe& qy) {
+    if (pub65) {
+        pub65[0] = ok ? 4 : 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            uint32_t xv = ok ? qx.v[7 - i] : 0u, yv = ok ? qy.v[7 - i] : 0u;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                pub65[1 + 4 * i + b] = (uint8_t)(xv >> (24 - 8 * b));
+                pub65[33 + 4 * i + b] = (uint8_t)(yv >> (24 - 8 * b));
+            }
+        }
+    }
+    if (addr20) {
+        uint32_t h[8];
+        keccak256_xy(h, qx.v, qy.v);
+        // hash bytes 12..31 = words 3..7 (little-endian byte order within words)
+#pragma unroll
+        for (int w = 3; w < 8; w++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) addr20[(w - 3) * 4 + b] = ok ? (uint8_t)(h[w] >> (8 * b)) : 0;
+    }
+}
+
+
+// ---------------------------------------------------------------------------- synthetic signer
+// Bench/test data generator (signing is not on the validation path): key_i, msg_i, nonce_i are
+// Keccak-256 of (le64(seed) || le64(i) || tag), keys/nonces reduced mod n (0 -> 1).
+GSV_DI void derive32(uint32_t out_be_limbs[8], uint64_t seed, uint64_t i, uint32_t tag3) {
+    uint64_t a[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) a[k] = 0;
+    a[0] = seed;
+    a[1] = i;
+    a[2] = (uint64_t)(tag3 & 0xFFFFFFu) | (0x01ull << 24);
+    a[16] = 0x8000000000000000ULL;
+    keccakf(a);
+    // hash bytes as a big-endian 256-bit number -> limbs
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        out_be_limbs[7 - 2 * j] = __builtin_bswap32((uint32_t)a[j]);
+        out_be_limbs[6 - 2 * j] = __builtin_bswap32((uint32_t)(a[j] >> 32));
+    }
+}
+
+// ECDSA signature with explicit nonce, low-s normalised (libsecp256k1 semantics); d, k are
+// reduced mod n here (0 -> 1).  (px, py) = d*G.  m = message as limbs (any 256-bit value).
+GSV_DI void ecdsa_sign(uint32_t r_out[8], uint32_t s_out[8], uint32_t& recid, fe& px, fe& py, sc d, sc k,
+                       const uint32_t m[8], const uint4* __restrict__ gtab) {
+    sc_cond_sub_n(d.v, d.v, 0);
+    sc_cond_sub_n(k.v, k.v, 0);
+    if (sc_is_zero(d)) d.v[0] = 1;
+    if (sc_is_zero(k)) k.v[0] = 1;
+    sc mr;
+    sc_cond_sub_n(mr.v, m, 0);
+    gej P;
+    bool pinf;
+    comb_mul_g(P, pinf, d, gtab);
+    fe zi, zi2;
+    fe_inv(zi, P.z);
+    fe_sqr(zi2, zi);
+    fe_mul(px, P.x, zi2);
+    fe_mul(zi2, zi2, zi);
+    fe_mul(py, P.y, zi2);
+    gej R;
+    bool rinf;
+    comb_mul_g(R, rinf, k, gtab);
+    fe rx, ry;
+    fe_inv(zi, R.z);
+    fe_sqr(zi2, zi);
+    fe_mul(rx, R.x, zi2);
+    fe_mul(zi2, zi2, zi);
+    fe_mul(ry, R.y, zi2);
+    recid = ry.v[0] & 1u;
+    sc r;
+    bool over = !limbs_lt(rx.v, SN);
+    sc_cond_sub_n(r.v, rx.v, 0);
+    if (over) recid |= 2u;
+    // s = k^-1 (m + r d)
+    sc kinv, s, t;
+    sc_inv(kinv, k);
+    sc_mul(t, r, d);
+    sc_add(t, t, mr);
+    sc_mul(s, kinv, t);
+    if (sc_is_high(s)) {
+        sc_neg(s, s);
+        recid ^= 1u;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        r_out[i] = r.v[i];
+        s_out[i] = s.v[i];
+    }
+}
+
+}  // namespace gsv

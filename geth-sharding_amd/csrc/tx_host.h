@@ -21,9 +21,4 @@ struct TxPrep {
 int tx_prepare(const uint8_t* rlp, size_t len, const uint8_t* chain_id, size_t chain_id_len,
                int signer_kind, TxPrep& out);
 
-// sharding/utils/marshal.go:144-198 Deserialize: blobs of a serialized collation body.
-// Appends (offset, length) pairs of each blob's data into `blobs` and the data into `data`.
-void blob_deserialize(const uint8_t* body, size_t len, std::vector<uint8_t>& data,
-                      std::vector<uint64_t>& blob_off);
-
 }  // namespace gsv

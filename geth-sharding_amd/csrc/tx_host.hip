@@ -233,28 +233,3 @@ int tx_prepare(const uint8_t* rlp, size_t len, const uint8_t* cid, size_t cidlen
 }
 
 }  // namespace gsv
-
-namespace gsv {
-
-void blob_deserialize(const uint8_t* body, size_t len, std::vector<uint8_t>& data,
-                      std::vector<uint64_t>& blob_off) {
-    size_t chunks = len / 32, parts = 0, cur = 0;
-    for (size_t i = 0; i < chunks; i++) {
-        int dl = body[i * 32] & 0x1F;  // getDatabyteLength (marshal.go:136-139)
-        if (dl == 0) {
-            parts++;
-            continue;
-        }
-        blob_off.push_back(data.size());
-        for (size_t c = 0; c < parts; c++) {
-            data.insert(data.end(), body + cur + 1, body + cur + 32);
-            cur += 32;
-        }
-        data.insert(data.end(), body + cur + 1, body + cur + 1 + dl);
-        cur += 32;
-        blob_off.push_back(data.size());
-        parts = 0;
-    }
-}
-
-}  // namespace gsv

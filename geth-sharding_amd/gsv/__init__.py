@@ -249,6 +249,57 @@ def _bn256_synth_checks_dev(self, seed, out_t, expect_t=None, stream=None):
         ctypes.c_void_p(expect_t.data_ptr()) if expect_t is not None else None, sp))
 
 
+def _tptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _notary_validate_shards(self, bodies, chain_id: int = 1, signer_kind: int = _lib.SIGNER_EIP155,
+                            max_txs: int = 8192, want_senders=True, want_status=True):
+    """Notary validation of collation bodies (gsv.h gsv_notary_validate_shards): returns
+    (roots (n,32), ntx (n,), bitmap (n, ceil(max_txs/8)), senders (n,max_txs,20) | None,
+    status (n,max_txs) | None)."""
+    n = len(bodies)
+    bm = (max_txs + 7) // 8
+    roots = np.zeros((n, 32), np.uint8)
+    ntx = np.zeros(n, np.uint32)
+    bitmap = np.zeros((n, bm), np.uint8)
+    senders = np.zeros((n, max_txs, 20), np.uint8) if want_senders else None
+    status = np.zeros((n, max_txs), np.uint8) if want_status else None
+    if n == 0:
+        return roots, ntx, bitmap, senders, status
+    flat, off = _pack(bodies)
+    cid = _be(chain_id)
+    cbuf = np.frombuffer(cid + b"\0", np.uint8)
+    check(_lib.load().gsv_notary_validate_shards(self._h, _ptr(flat), _ptr(off), n, _ptr(cbuf), len(cid),
+                                                 int(signer_kind), int(max_txs), _ptr(roots), _ptr(ntx),
+                                                 _ptr(bitmap), _ptr(senders), _ptr(status)))
+    return roots, ntx, bitmap, senders, status
+
+
+def _notary_validate_shards_dev(self, bodies_t, h_off, roots_t, ntx_t, bitmap_t, senders_t=None, status_t=None,
+                                chain_id: int = 1, signer_kind: int = _lib.SIGNER_EIP155, max_txs: int = 8192,
+                                stream=None):
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    n = h_off.shape[0] - 1
+    cid = _be(chain_id)
+    cbuf = np.frombuffer(cid + b"\0", np.uint8)
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_notary_validate_shards_dev(self._h, _tptr(bodies_t), _ptr(h_off), n, _ptr(cbuf), len(cid),
+                                                     int(signer_kind), int(max_txs), _tptr(roots_t), _tptr(ntx_t),
+                                                     _tptr(bitmap_t), _tptr(senders_t), _tptr(status_t), sp))
+
+
+def _notary_synth_dev(self, seed, shard0, n_shards, txs_per_shard, bodies_t, exp_status_t=None, exp_sender_t=None,
+                      stream=None):
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_notary_synth_dev(self._h, ctypes.c_uint64(seed), int(shard0), int(n_shards),
+                                           int(txs_per_shard), _tptr(bodies_t), _tptr(exp_status_t),
+                                           _tptr(exp_sender_t), sp))
+
+
+Context.notary_validate_shards = _notary_validate_shards
+Context.notary_validate_shards_dev = _notary_validate_shards_dev
+Context.notary_synth_dev = _notary_synth_dev
 Context.bn256_synth_checks_dev = _bn256_synth_checks_dev
 Context.pairing_check_batch = _pairing_check_batch
 Context.pairing_check_batch_dev = _pairing_check_batch_dev

@@ -41,6 +41,7 @@ K_PAIRING = 4
 K_SENDER_PREP = 5
 K_BN_PREPARE = 6
 K_BN_FINAL = 7
+K_NOTARY = 8
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -72,8 +73,12 @@ SIGNATURES = [
     ("gsv_bn256_synth_checks_dev", ctypes.c_int, [_vp, ctypes.c_uint64, _sz, _vp, _vp, _vp]),
     ("gsv_synth_sign", ctypes.c_int, [_vp, ctypes.c_uint64, _sz, _vp, _vp, _vp, _vp]),
     ("gsv_synth_sign_dev", ctypes.c_int, [_vp, ctypes.c_uint64, _sz, _vp, _vp, _vp, _vp, _vp]),
-    ("gsv_notary_validate_shards", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, ctypes.c_uint32,
-                                                  _vp, _vp, _vp, _vp]),
+    ("gsv_notary_validate_shards", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, ctypes.c_int, ctypes.c_uint32,
+                                                  _vp, _vp, _vp, _vp, _vp]),
+    ("gsv_notary_validate_shards_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, ctypes.c_int,
+                                                      ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("gsv_notary_synth_dev", ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32, _sz, ctypes.c_uint32, _vp, _vp,
+                                            _vp, _vp]),
 ]
 
 _lib = None

@@ -97,7 +97,8 @@ int gsv_ctx_set_timing(gsv_ctx *ctx, int enable);
 #define GSV_K_SENDER_PREP 5
 #define GSV_K_BN_PREPARE 6 /* pair decode + G1 curve + G2 subgroup checks */
 #define GSV_K_BN_FINAL 7   /* per-check product + final exponentiation */
-#define GSV_K_COUNT 8
+#define GSV_K_NOTARY 8     /* blob index + per-tx decode/sighash/recover of the notary path */
+#define GSV_K_COUNT 12
 /* total milliseconds and launch count accumulated for kernel `kid` since the last reset */
 int gsv_ctx_kernel_time(gsv_ctx *ctx, int kid, double *total_ms, long *launches);
 int gsv_ctx_reset_timing(gsv_ctx *ctx);
@@ -169,15 +170,32 @@ int gsv_synth_sign_dev(gsv_ctx *ctx, uint64_t seed, size_t n, uint8_t *d_msg32, 
 int gsv_bn256_synth_checks_dev(gsv_ctx *ctx, uint64_t seed, size_t nchecks, uint8_t *d_out768,
                                uint8_t *d_expect, void *stream);
 
-/* ---- notary validation of whole collations (Cfg4) ----
- * For each shard body: blob-deserialize (sharding/utils/marshal.go:144-198), RLP-decode each tx,
- * recover every sender (EIP-155 signer with chain_id), and compute the chunk root.
- * Outputs per shard: root32, tx count, and a validity bitmap of max_txs bits (bit t = tx t
- * recovered OK); senders (optional) n_total x 20 B in shard order. */
-int gsv_notary_validate_shards(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off,
-                               size_t n_shards, const uint8_t *chain_id, size_t chain_id_len,
-                               uint32_t max_txs, uint8_t *root32_out, uint32_t *ntx_out,
-                               uint8_t *valid_bitmap_out, uint8_t *senders_out);
+/* ---- notary validation of whole collations (configs[3]) ----
+ * Shard s body = bodies[off[s] .. off[s+1]), at most 2^20 bytes (sharding/collation.go:45).  On the
+ * GPU: blob-deserialize (sharding/utils/marshal.go:144-198), decode every blob as an RLP transaction
+ * and recover its sender with the signer (GSV_SIGNER_*, chain_id big-endian; the reference notary's
+ * chain uses EIP-155), and compute the chunk root (sharding/collation.go:115-119).
+ * Per shard: root32_out[32], ntx_out = number of blobs, valid_bitmap_out[(max_txs+7)/8] with bit t
+ * (LSB first) set when tx t's sender recovered (GSV_ST_OK).  Optional per tx, laid out
+ * [n_shards][max_txs]: senders_out (20 B, zero when not OK) and status_out (GSV_ST_*).
+ * A shard with more than max_txs blobs: only the first max_txs are validated; the host entry point
+ * returns GSV_E_TOO_LARGE for it (the _dev one reports it through ntx > max_txs). */
+int gsv_notary_validate_shards(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off, size_t n_shards,
+                               const uint8_t *chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
+                               uint8_t *root32_out, uint32_t *ntx_out, uint8_t *valid_bitmap_out,
+                               uint8_t *senders_out, uint8_t *status_out);
+/* Device-resident form: d_bodies/outputs in HBM, h_off on the host; enqueues on `stream`. */
+int gsv_notary_validate_shards_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off, size_t n_shards,
+                                   const uint8_t *chain_id, size_t chain_id_len, int signer_kind,
+                                   uint32_t max_txs, uint8_t *d_root32, uint32_t *d_ntx, uint8_t *d_bitmap,
+                                   uint8_t *d_senders, uint8_t *d_status, void *stream);
+
+/* ---- synthetic collations (bench / test data; configs[3]) ----
+ * Bodies of shards shard0 .. shard0+n_shards-1 (txs_per_shard x 128 B each, contiguous): signed
+ * EIP-155 txs (chain id 1) blob-serialized 4 chunks per tx; every 128th tx invalid by construction
+ * (high-s / wrong chain id / r not an x-coordinate).  Optional expected status and sender per tx. */
+int gsv_notary_synth_dev(gsv_ctx *ctx, uint64_t seed, uint32_t shard0, size_t n_shards, uint32_t txs_per_shard,
+                         uint8_t *d_bodies, uint8_t *d_exp_status, uint8_t *d_exp_sender, void *stream);
 
 #ifdef __cplusplus
 }
