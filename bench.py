@@ -50,6 +50,21 @@ PERMS_PER_MIB = 83016      # Keccak-f permutations per 1 MiB chunk root (SURVEY.
 HBM_PEAK_GBPS = 8000.0
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc", "pmc_summary.json")
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this bench
+    (tools/profile_round.sh -> tools/pmc_summary.py): FETCH_SIZE x 2 (gfx950 correction,
+    MI355X_MICROARCH.md § HBM) + WRITE_SIZE.  None when no summary is committed."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            k = json.load(f)[kernel]
+        return int(k["fetch_bytes_x2"] + k["write_bytes"]), os.path.relpath(PMC_SUMMARY, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def dist_setup():
     import torch
     ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -357,6 +372,7 @@ def main():
 
     if rank == 0:
         achieved = MACS_PER_RECOVERY * N_SIGS / (k_avg_ms * 1e-3)
+        traffic, traffic_src = pmc_traffic("gsv::k_ecrecover")
         line = {
             "metric": "ecrecover sigs/sec + Keccak collation GB/s",
             "value": round(sigs_per_s, 1),
@@ -374,7 +390,9 @@ def main():
                                    "per GPU (BASELINE.json configs[1])",
                        "signatures_per_gpu": N_SIGS, "parallelism": f"shard-partitioned x{ws}"},
             "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_MAC / 1e12, 3),
-                         "unit": "TMAC/s", "frac": round(achieved / PEAK_MAC, 4), "traffic": None,
+                         "unit": "TMAC/s", "frac": round(achieved / PEAK_MAC, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": N_SIGS * (32 + 65 + 65 + 20 + 1),
                          "kernel": "k_ecrecover", "kernel_avg_ms": round(k_avg_ms, 4),
                          "algorithmic_per_unit": f"{MACS_PER_RECOVERY} 32x32-bit partial products per recovery"},
             "cpu_baseline": cpu,

@@ -76,8 +76,11 @@ def main(root):
             busy = per_dispatch(s["SQ_BUSY_CYCLES"]) if s.get("SQ_BUSY_CYCLES") else None
             act = per_dispatch(s["SQ_ACTIVE_INST_VALU"]) if s.get("SQ_ACTIVE_INST_VALU") else None
             wcyc = per_dispatch(s["SQ_WAVE_CYCLES"]) if s.get("SQ_WAVE_CYCLES") else None
-            if act and wcyc:
-                r["valu_active_frac_of_wave_cycles"] = round(act / wcyc, 4)
+            gui = per_dispatch(s["GRBM_GUI_ACTIVE"]) if s.get("GRBM_GUI_ACTIVE") else None
+            if gui:
+                # GRBM_GUI_ACTIVE sums the 8 XCDs' clocks; each of the 1024 SIMDs issues at most one
+                # wave-instruction per cycle: VALU wave-instructions per SIMD per cycle
+                r["valu_issue_per_simd_cycle"] = round(r["sq_insts_valu"] / (1024 * gui / 8), 4)
         res[k] = r
     json.dump(res, sys.stdout, indent=1, sort_keys=True)
     print()
