@@ -186,7 +186,20 @@ static BN_NI void g2_add_p(g2j* pc, const g2j* pa, const g2j* pb) {
     c = o;
 }
 GSV_DI void g2_add(g2j& c, const g2j& a, const g2j& b) { g2_add_p(&c, &a, &b); }
-// twist.go:47-63: y^2 == x^3 + 3/xi and Order * Q == infinity (twist.go:164-176 double-and-add)
+// psi(X : Y : Z) = (conj(X) xi^((p-1)/3) : conj(Y) xi^((p-1)/2) : conj(Z)) — the p-power
+// Frobenius carried through the twist isomorphism (optate.go:173-176 applies it to affine Q)
+GSV_DI void g2_psi(g2j& o, const g2j& a) {
+    fp2 k, c;
+    fp2_conj(c, a.x);
+    fp2_const(k, XI_P1_3_X, XI_P1_3_Y);
+    fp2_mul(o.x, c, k);
+    fp2_conj(c, a.y);
+    fp2_const(k, XI_P1_2_X, XI_P1_2_Y);
+    fp2_mul(o.y, c, k);
+    fp2_conj(o.z, a.z);
+    o.t = a.t;
+}
+// twist.go:47-63: y^2 == x^3 + 3/xi and Q in the order-r subgroup
 static BN_NI bool g2_in_subgroup(const g2a* q) {
     fp2 y2, x3, b;
     fp2_sqr(y2, q->y);
@@ -195,22 +208,39 @@ static BN_NI bool g2_in_subgroup(const g2a* q) {
     fp2_const(b, TWIST_B_X, TWIST_B_Y);
     fp2_add(x3, x3, b);
     if (!fp2_eq(y2, x3)) return false;
-    g2j a, sum;
+    // The reference decides membership with Order*Q == infinity (twist.go:60-62, 254-bit
+    // double-and-add).  We decide the same predicate with the endomorphism psi (the
+    // untwist-Frobenius-twist map the Miller loop already uses for Q1, optate.go:173-176):
+    //   [r]Q == O  <=>  [u+1]Q + psi([u]Q) + psi^2([u]Q) == psi^3([2u]Q)
+    // for every Q on E'(F_p^2) of BN254 (Dai-Lin-Zhao-Zhou, eprint 2022/348, sec. 3 and 5.1):
+    // a 63-bit multiplication instead of a 254-bit one.  Checked against the oracle's
+    // Order*Q on random points inside and outside G2 (tests/test_gpu_bn256.py).
+    g2j a;
     a.x = q->x;
     a.y = q->y;
     fp2_one(a.z);
     fp2_one(a.t);
-    // Order has bit length 254: the reference's loop starts at bit 254 (always 0) on the zero
-    // point; starting from sum = Q at bit 253 gives the same group element.
-    sum = a;
+    g2j uq = a;  // [u]Q, u = 4965661367192848881 (63 bits, top bit set)
 #pragma unroll 1
-    for (int i = 252; i >= 0; i--) {
+    for (int i = 61; i >= 0; i--) {
         g2j t;
-        g2_double(t, sum);
-        if ((BN_ORDER[i >> 5] >> (i & 31)) & 1u) g2_add(sum, t, a);
-        else sum = t;
+        g2_double(t, uq);
+        if ((BN_U >> i) & 1) g2_add(uq, t, a);
+        else uq = t;
     }
-    return fp2_is_zero(sum.z);
+    g2j lhs, p1, p2, rhs, tmp;
+    g2_add(lhs, uq, a);          // [u+1]Q
+    g2_psi(p1, uq);              // psi([u]Q)
+    g2_psi(p2, p1);              // psi^2([u]Q)
+    g2_add(lhs, lhs, p1);
+    g2_add(lhs, lhs, p2);
+    g2_double(tmp, uq);          // [2u]Q
+    g2_psi(rhs, tmp);
+    g2_psi(rhs, rhs);
+    g2_psi(rhs, rhs);            // psi^3([2u]Q)
+    fp2_neg(rhs.y, rhs.y);
+    g2_add(tmp, lhs, rhs);       // lhs - rhs
+    return fp2_is_zero(tmp.z);
 }
 
 // ---------------------------------------------------------------- Miller loop (optate.go)

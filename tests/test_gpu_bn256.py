@@ -124,3 +124,28 @@ def test_synth_checks_match_oracle(ctx, oracle):
     v = ctx.pairing_check_batch([bytes(r) for r in h])
     assert (v == e).all()
     assert (e == 1).sum() and (e == 0).sum() and (e == 2).sum() == 1
+
+
+def test_g2_subgroup_predicate_vs_oracle(ctx, oracle):
+    """The GPU decides G2 membership with the psi-endomorphism criterion; the oracle with the
+    reference's Order*Q double-and-add (twist.go:60-62).  Both must classify identically: random
+    twist points outside G2, pure cofactor-order points [r]X, mixed points X + G, and G2 points."""
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    import bn254_py as B
+    rng = random.Random(23)
+    g1 = oracle.bn256_g1_mul(1)
+    pts = []
+    for k in range(48):
+        x = B.twist_point_outside_g2(rng.randrange(1, 1 << 60))
+        pts.append(x)
+        if k < 6:
+            pts.append(B.g2_mul(x, B.R))                              # order divides the cofactor
+            pts.append(B.g2_add(x, B.g2_decode(oracle.bn256_g2_mul(rng.randrange(1, R)))))  # mixed
+    for _ in range(16):
+        pts.append(B.g2_decode(oracle.bn256_g2_mul(rng.randrange(1, R))))  # in G2
+    inputs = [g1 + B.g2_encode(p) for p in pts if p is not None]
+    out = ctx.pairing_check_batch(inputs)
+    want = [_v(oracle, x) for x in inputs]
+    assert list(out) == want
+    assert want.count(2) >= 48 and want.count(0) >= 16  # e(G, Q) != 1 for Q in G2 \ {O}
