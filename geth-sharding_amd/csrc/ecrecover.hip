@@ -10,7 +10,7 @@
 //   core/types/transaction_signing.go:222-247 recoverPlain + crypto/crypto.go:181-192 (sender kernel)
 //
 // Algorithm (ours, MI355X-first — not libsecp256k1's Strauss-wNAF, which branches per digit and
-// wastes SIMD lanes):
+// wastes SIMD lanes).  Field arithmetic: 9 x 29-bit limbs with lazy reduction (secp256k1_fe9.cuh).
 //   * u2*R: GLV split u2 = k1 + k2*lambda (|k1|,|k2| < 2^128), fixed-schedule odd-digit w=3
 //     recoding (every 3rd bit adds, identical across the wave: no divergence), 4-entry table
 //     {1,3,5,7}R built on an isomorphic curve (libsecp-style "global z") so all table points are
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
 
 // recoverPlain (core/types/transaction_signing.go:222-247) + ValidateSignatureValues
 // (crypto/crypto.go:181-192) + address = Keccak256(pub[1:])[12:]
-__global__ __launch_bounds__(256) void k_sender(const uint8_t* __restrict__ sighash32,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAVES, GSV_ECR_WAVES))) void k_sender(const uint8_t* __restrict__ sighash32,
                                                 const uint8_t* __restrict__ r32,
                                                 const uint8_t* __restrict__ s32,
                                                 const uint64_t* __restrict__ v,
@@ -85,41 +85,42 @@ __global__ __launch_bounds__(256) void k_sender(const uint8_t* __restrict__ sigh
     status[i] = (uint8_t)st;
 }
 
-// Fixed-base comb table: entry (w, d) = d * 2^(8w) * G, affine, for d = 1..255 (d = 0 -> G, unused)
+// Fixed-base comb table: entry (w, d) = d * 2^(8w) * G, affine, canonical fe9 limbs
+// (x[9] y[9] + 2 pad words, recover_dev.cuh gtab_load), for d = 1..255 (d = 0 -> G, unused)
 __global__ __launch_bounds__(256) void k_gtable_init(uint4* __restrict__ gtab) {
     uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= 32 * 256) return;
     uint32_t w = id >> 8, d = id & 255u;
     if (d == 0) d = 1;
-    ge G;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        G.x.v[i] = GX[i];
-        G.y.v[i] = GY[i];
-    }
+    ge9 G;
+    fe9_from_const(G.x, GX);
+    fe9_from_const(G.y, GY);
     // scalar d << 8w, double-and-add from the top bit
-    gej acc;
+    gej9 acc;
     bool inf = true;
     acc.x = G.x;
     acc.y = G.y;
-    fe_set_u32(acc.z, 1);
+    fe9_set_u32(acc.z, 1);
     int top = 8 * (int)w + 7;
     for (int b = top; b >= 0; b--) {
-        if (!inf) gej_dbl(acc, acc);
+        if (!inf) gej9_dbl(acc, acc);
         int bit = (b >= 8 * (int)w) ? (int)((d >> (b - 8 * (int)w)) & 1u) : 0;
-        if (bit) gej_add_ge(acc, inf, acc, G);
+        if (bit) gej9_add_ge(acc, inf, acc, G);
     }
-    fe zi, zi2, x, y;
-    fe_inv(zi, acc.z);
-    fe_sqr(zi2, zi);
-    fe_mul(x, acc.x, zi2);
-    fe_mul(zi2, zi2, zi);
-    fe_mul(y, acc.y, zi2);
-    uint4* e = gtab + (size_t)id * 4;
+    fe9 zi, zi2, x, y;
+    fe9_inv(zi, acc.z);
+    fe9_sqr(zi2, zi);
+    fe9_mul(x, acc.x, zi2);
+    fe9_mul(zi2, zi2, zi);
+    fe9_mul(y, acc.y, zi2);
+    fe9_normalize_full(x);
+    fe9_normalize_full(y);
+    uint4* e = gtab + (size_t)id * GTAB_ENTRY_U4;
     e[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
     e[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
-    e[2] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
-    e[3] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
+    e[2] = make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]);
+    e[3] = make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]);
+    e[4] = make_uint4(y.v[7], y.v[8], 0u, 0u);
 }
 
 // ---------------------------------------------------------------------------- synthetic signer

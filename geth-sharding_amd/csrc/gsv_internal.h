@@ -52,6 +52,7 @@ hipError_t launch_notary_synth(uint64_t seed, uint32_t shard0, uint32_t n_shards
                                hipStream_t st);
 
 constexpr size_t GTAB_ENTRIES = 32 * 256;
-constexpr size_t GTAB_BYTES = GTAB_ENTRIES * 64;
+constexpr size_t GTAB_ENTRY_BYTES = 80;  // fe9 x[9] y[9] + 2 pad words (recover_dev.cuh gtab_load)
+constexpr size_t GTAB_BYTES = GTAB_ENTRIES * GTAB_ENTRY_BYTES;
 
 }  // namespace gsv

@@ -4,6 +4,10 @@
 #include "gsv_internal.h"
 #include "keccak_dev.cuh"
 #include "secp256k1_dev.cuh"
+// the rare p == q doubling of the mixed add runs out of line (see gej9_dbl_ool below)
+namespace gsv { struct gej9; __device__ void gej9_dbl_rare(gej9& o, const gej9& p); }
+#define GEJ9_DBL_RARE(o, p) gej9_dbl_rare(o, p)
+#include "secp256k1_fe9.cuh"
 
 namespace gsv {
 
@@ -28,6 +32,11 @@ __device__ constexpr uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75F
 __device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
                                            0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
 
+// GSV_LX_TABLE=1 keeps the four lambda-table x-coordinates (beta * x) in registers (36 VGPRs);
+// 0 recomputes beta * x per lambda add (+44 field products, no spills at 2 waves/SIMD)
+#ifndef GSV_LX_TABLE
+#define GSV_LX_TABLE 0
+#endif
 constexpr int GLV_DIGITS = 44;  // w = 3 odd digits cover k < 2^131 (bound is 2^128)
 
 // ---------------------------------------------------------------------------- scalar helpers
@@ -39,7 +48,7 @@ GSV_DI void sc_from_const(sc& r, const uint32_t c[8]) {
 // (k * g) >> 272, rounded (libsecp256k1 scalar_8x32_impl.h mul_shift_var semantics)
 GSV_DI void sc_mul_shift272(sc& r, const sc& k, const uint32_t g[8]) {
     uint32_t t[16];
-    mul_8x8_asm(t, k.v, g);
+    mul_8x8_fx(t, k.v, g);
 #pragma unroll
     for (int i = 0; i < 7; i++) r.v[i] = (t[8 + i] >> 16) | (t[9 + i] << 16);
     r.v[7] = t[15] >> 16;
@@ -111,124 +120,120 @@ GSV_DI void recode_w3(uint32_t dig[6], uint32_t& skew, const sc& kin) {
 }
 
 // ---------------------------------------------------------------------------- group helpers
-GSV_DI void ge_cmov(ge& r, const ge& a, bool f) {
-    fe_cmov(r.x, a.x, f);
-    fe_cmov(r.y, a.y, f);
+// Field elements are fe9 (secp256k1_fe9.cuh); the magnitude of every intermediate is noted.
+GSV_DI void fe9_from_const(fe9& r, const uint32_t c[8]) {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = c[i];
+    fe9_from_words(r, w);
+}
+GSV_DI void ge9_cmov(ge9& r, const ge9& a, bool f) {
+    fe9_cmov(r.x, a.x, f);
+    fe9_cmov(r.y, a.y, f);
 }
 
-// mixed add with the z-ratio output (no exceptional cases possible where it is used)
-GSV_DI void gej_add_ge_zr(gej& r, fe& zr, const gej& p, const ge& q) {
-    fe z1z1, u2, s2, h, hh, i4, j, rr, v, t;
-    fe_sqr(z1z1, p.z);
-    fe_mul(u2, q.x, z1z1);
-    fe_mul(s2, q.y, p.z);
-    fe_mul(s2, s2, z1z1);
-    fe_sub(h, u2, p.x);
-    fe_sub(rr, s2, p.y);
-    fe_sqr(hh, h);
-    fe_add(i4, hh, hh);
-    fe_add(i4, i4, i4);
-    fe_mul(j, h, i4);
-    fe_add(rr, rr, rr);
-    fe_mul(v, p.x, i4);
-    gej o;
-    fe_sqr(t, rr);
-    fe_sub(t, t, j);
-    fe_sub(t, t, v);
-    fe_sub(o.x, t, v);
-    fe_sub(t, v, o.x);
-    fe_mul(t, rr, t);
-    fe_mul(v, p.y, j);
-    fe_add(v, v, v);
-    fe_sub(o.y, t, v);
-    fe_add(t, p.z, h);
-    fe_sqr(t, t);
-    fe_sub(t, t, z1z1);
-    fe_sub(o.z, t, hh);
-    fe_add(zr, h, h);  // Z3 = 2 * Z1 * H
-    r = o;
+// Doubling for the rare p == q case of the mixed add, out of line so the hot loops stay small
+// in I-cache; the point travels in VGPR vectors (an aggregate or pointer argument would pin the
+// caller's accumulator to scratch memory).
+typedef uint32_t gsv_v32 __attribute__((ext_vector_type(32)));
+__device__ __noinline__ gsv_v32 gej9_dbl_ool(gsv_v32 in) {
+    gej9 p, d;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        p.x.v[i] = in[i];
+        p.y.v[i] = in[9 + i];
+        p.z.v[i] = in[18 + i];
+    }
+    gej9_dbl(d, p);
+    gsv_v32 o;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        o[i] = d.x.v[i];
+        o[9 + i] = d.y.v[i];
+        o[18 + i] = d.z.v[i];
+    }
+#pragma unroll
+    for (int i = 27; i < 32; i++) o[i] = 0;
+    return o;
+}
+__device__ void gej9_dbl_rare(gej9& o, const gej9& p) {
+    gsv_v32 in;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        in[i] = p.x.v[i];
+        in[9 + i] = p.y.v[i];
+        in[18 + i] = p.z.v[i];
+    }
+#pragma unroll
+    for (int i = 27; i < 32; i++) in[i] = 0;
+    gsv_v32 d = gej9_dbl_ool(in);
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        o.x.v[i] = d[i];
+        o.y.v[i] = d[9 + i];
+        o.z.v[i] = d[18 + i];
+    }
 }
 
-// (X, Y) scaled to Z * f: (X f^2, Y f^3)
-GSV_DI void scale_xy(ge& r, const fe& x, const fe& y, const fe& f) {
-    fe f2, f3;
-    fe_sqr(f2, f);
-    fe_mul(f3, f2, f);
-    fe_mul(r.x, x, f2);
-    fe_mul(r.y, y, f3);
-}
-
-// Odd multiples {1,3,5,7}R as affine points of an isomorphic curve E'' (no inversion);
-// a Jacobian result (X,Y,Z) on E'' is (X, Y, Z * zfac) on E.
-GSV_DI void build_r_table(ge T[4], fe& zfac, const fe& x, const fe& y) {
-    gej R1;
-    R1.x = x;
-    R1.y = y;
-    fe_set_u32(R1.z, 1);
-    gej D;
-    gej_dbl(D, R1);
-    fe u2, u3;
-    fe_sqr(u2, D.z);
-    fe_mul(u3, u2, D.z);
-    ge Dp;
-    Dp.x = D.x;
-    Dp.y = D.y;
-    gej P1, P3, P5, P7;
-    fe_mul(P1.x, x, u2);
-    fe_mul(P1.y, y, u3);
-    fe_set_u32(P1.z, 1);
-    fe zr3, zr5, zr7;
-    gej_add_ge_zr(P3, zr3, P1, Dp);
-    gej_add_ge_zr(P5, zr5, P3, Dp);
-    gej_add_ge_zr(P7, zr7, P5, Dp);
-    T[3].x = P7.x;
-    T[3].y = P7.y;
-    scale_xy(T[2], P5.x, P5.y, zr7);
-    fe f;
-    fe_mul(f, zr5, zr7);
-    scale_xy(T[1], P3.x, P3.y, f);
-    fe_mul(f, f, zr3);
-    scale_xy(T[0], P1.x, P1.y, f);
-    fe_mul(zfac, D.z, P7.z);
-}
-
-GSV_DI void table_select(ge& out, const ge T[4], uint32_t idx) {
+GSV_DI void table_select9(ge9& out, const ge9 T[4], uint32_t idx) {
     out = T[0];
 #pragma unroll
-    for (int e = 1; e < 4; e++) ge_cmov(out, T[e], idx == (uint32_t)e);
+    for (int e = 1; e < 4; e++) ge9_cmov(out, T[e], idx == (uint32_t)e);
 }
-GSV_DI void table_select_x(fe& out, const fe X[4], uint32_t idx) {
+GSV_DI void table_select9_x(fe9& out, const fe9 X[4], uint32_t idx) {
     out = X[0];
 #pragma unroll
-    for (int e = 1; e < 4; e++) fe_cmov(out, X[e], idx == (uint32_t)e);
+    for (int e = 1; e < 4; e++) fe9_cmov(out, X[e], idx == (uint32_t)e);
 }
 
-// u*G with the byte-window comb table (gtab[w*256 + d] = d * 2^(8w) * G, affine, 16 words)
-GSV_DI void comb_mul_g(gej& acc, bool& inf, const sc& u, const uint4* __restrict__ gtab) {
+// comb table entry (w, d) = d * 2^(8w) * G, affine, canonical fe9 limbs: x[9] y[9] + 2 pad words
+constexpr int GTAB_ENTRY_U4 = GTAB_ENTRY_BYTES / 16;
+GSV_DI void gtab_load(ge9& P, const uint4* e) {
+    uint4 a = e[0], b = e[1], c = e[2], d = e[3], f = e[4];
+    uint32_t w[20] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w,
+                      d.x, d.y, d.z, d.w, f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        P.x.v[i] = w[i];
+        P.y.v[i] = w[9 + i];
+    }
+}
+
+// u*G with the byte-window comb table (32 mixed adds, no doublings)
+GSV_DI void comb_mul_g9(gej9& acc, bool& inf, const sc& u, const uint4* __restrict__ gtab) {
     inf = true;
-    const uint4* e = gtab + (size_t)(u.v[0] & 0xFFu) * 4;
-    uint4 n0 = e[0], n1 = e[1], n2 = e[2], n3 = e[3];
+    ge9 Pn;
+    gtab_load(Pn, gtab + (size_t)(u.v[0] & 0xFFu) * GTAB_ENTRY_U4);
 #pragma unroll 1
     for (int w = 0; w < 32; w++) {
         uint32_t d = (sel_word(u.v, (uint32_t)w >> 2) >> ((w & 3) * 8)) & 0xFFu;
-        ge P;
-        P.x.v[0] = n0.x; P.x.v[1] = n0.y; P.x.v[2] = n0.z; P.x.v[3] = n0.w;
-        P.x.v[4] = n1.x; P.x.v[5] = n1.y; P.x.v[6] = n1.z; P.x.v[7] = n1.w;
-        P.y.v[0] = n2.x; P.y.v[1] = n2.y; P.y.v[2] = n2.z; P.y.v[3] = n2.w;
-        P.y.v[4] = n3.x; P.y.v[5] = n3.y; P.y.v[6] = n3.z; P.y.v[7] = n3.w;
+        ge9 P = Pn;
         if (w < 31) {  // prefetch next window's entry
             uint32_t dn = (sel_word(u.v, (uint32_t)(w + 1) >> 2) >> (((w + 1) & 3) * 8)) & 0xFFu;
-            const uint4* en = gtab + ((size_t)(w + 1) * 256 + dn) * 4;
-            n0 = en[0]; n1 = en[1]; n2 = en[2]; n3 = en[3];
+            gtab_load(Pn, gtab + ((size_t)(w + 1) * 256 + dn) * GTAB_ENTRY_U4);
         }
-        gej t;
+        gej9 t;
         bool tinf = inf;
-        gej_add_ge(t, tinf, acc, P);
+        gej9_add_ge(t, tinf, acc, P);
         if (d != 0) {
             acc = t;
             inf = tinf;
         }
     }
+}
+
+// Jacobian -> affine canonical 8 x 32-bit words
+GSV_DI void gej9_to_affine_words(fe& ax, fe& ay, const gej9& q) {
+    fe9 zi, zi2, x, y;
+    fe9_inv(zi, q.z);
+    fe9_sqr(zi2, zi);
+    fe9_mul(x, q.x, zi2);
+    fe9_mul(zi2, zi2, zi);
+    fe9_mul(y, q.y, zi2);
+    fe9_normalize_full(x);
+    fe9_normalize_full(y);
+    fe9_to_words(ax.v, x);
+    fe9_to_words(ay.v, y);
 }
 
 // ---------------------------------------------------------------------------- recovery core
@@ -247,29 +252,31 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     sc_cond_sub_n(m.v, msg, 0);  // msg mod n (msg < 2^256 < 2n)
 
     // x = r (+ n when recid & 2; fails for r >= p - n)
-    fe x;
+    fe9 x;
     {
         bool hi = (recid & 2u) != 0;
         ok = ok && (!hi || limbs_lt(r, P_MINUS_N));
+        uint32_t xw[8];
         uint64_t c = 0;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             c = (uint64_t)r[i] + (hi ? SN[i] : 0u) + hi32(c);
-            x.v[i] = lo32(c);
+            xw[i] = lo32(c);
         }
+        fe9_from_words(x, xw);
     }
     // y = sqrt(x^3 + 7), parity recid & 1
-    fe y, t;
-    fe_sqr(t, x);
-    fe_mul(t, t, x);
-    fe seven;
-    fe_set_u32(seven, 7);
-    fe_add(t, t, seven);
-    ok = ok && fe_sqrt(y, t);
+    fe9 y, t;
+    fe9_sqr(t, x);
+    fe9_mul(t, t, x);
+    t.v[0] += 7u;
+    ok = ok && fe9_sqrt(y, t);
     {
-        fe ny;
-        fe_neg(ny, y);
-        fe_cmov(y, ny, (y.v[0] & 1u) != (recid & 1u));
+        fe9_normalize_full(y);
+        fe9 ny;
+        fe9_neg<1>(ny, y);
+        fe9_normalize_weak(ny);
+        fe9_cmov(y, ny, (y.v[0] & 1u) != (recid & 1u));
     }
     // u1 = -m / r, u2 = s / r
     sc rn, u1, u2;
@@ -295,28 +302,29 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     recode_w3(dig1, skew1, k1);
     recode_w3(dig2, skew2, k2);
 
-    ge T[4];
-    fe zfac;
-    build_r_table(T, zfac, x, y);
-    fe LX[4];
+    ge9 T[4];
+    fe9 zfac;
+    build_r_table9(T, zfac, x, y);
+#if GSV_LX_TABLE
+    fe9 LX[4];
     {
-        fe beta;
+        fe9 beta;
+        fe9_from_const(beta, BETA);
 #pragma unroll
-        for (int i = 0; i < 8; i++) beta.v[i] = BETA[i];
-#pragma unroll
-        for (int e = 0; e < 4; e++) fe_mul(LX[e], T[e].x, beta);
+        for (int e = 0; e < 4; e++) fe9_mul(LX[e], T[e].x, beta);
     }
+#endif
 
-    gej acc;
+    gej9 acc;
     bool ainf = true;
     acc.x = T[0].x;
     acc.y = T[0].y;
-    fe_set_u32(acc.z, 1);
+    fe9_set_u32(acc.z, 1);
 #pragma unroll 1
     for (int i = GLV_DIGITS - 1; i >= 0; i--) {
         if (i != GLV_DIGITS - 1) {
 #pragma unroll 1
-            for (int d = 0; d < 3; d++) gej_dbl(acc, acc);
+            for (int d = 0; d < 3; d++) gej9_dbl(acc, acc);
         }
         uint32_t c1 = (sel_word(dig1, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
         uint32_t c2 = (sel_word(dig2, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
@@ -325,15 +333,23 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         for (int j = 0; j < 2; j++) {
             uint32_t c = j ? c2 : c1;
             bool ng = j ? neg2 : neg1;
-            ge P;
-            table_select(P, T, c & 3u);
-            fe lx;
-            table_select_x(lx, LX, c & 3u);
-            fe_cmov(P.x, lx, j != 0);
-            fe ny;
-            fe_neg(ny, P.y);
-            fe_cmov(P.y, ny, ((c >> 3) != 0) != ng);
-            gej_add_ge(acc, ainf, acc, P);
+            ge9 P;
+            table_select9(P, T, c & 3u);
+#if GSV_LX_TABLE
+            fe9 lx;
+            table_select9_x(lx, LX, c & 3u);
+            fe9_cmov(P.x, lx, j != 0);
+#else
+            if (j != 0) {  // lambda(x, y) = (beta x, y); wave-uniform branch
+                fe9 beta;
+                fe9_from_const(beta, BETA);
+                fe9_mul(P.x, P.x, beta);
+            }
+#endif
+            fe9 ny;
+            fe9_neg<1>(ny, P.y);         // 2
+            fe9_cmov(P.y, ny, ((c >> 3) != 0) != ng);
+            gej9_add_ge(acc, ainf, acc, P);
         }
     }
     // skew corrections: the recoded scalars were k + skew -> subtract (+-)T0 / (+-)lambda(T0)
@@ -341,38 +357,40 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     for (int j = 0; j < 2; j++) {
         bool ng = j ? neg2 : neg1;
         uint32_t sk = j ? skew2 : skew1;
-        ge P;
+        ge9 P;
         P.x = T[0].x;
-        fe_cmov(P.x, LX[0], j != 0);
-        fe_neg(P.y, T[0].y);
-        fe_cmov(P.y, T[0].y, ng);
-        gej tmp;
+#if GSV_LX_TABLE
+        fe9_cmov(P.x, LX[0], j != 0);
+#else
+        if (j != 0) {
+            fe9 beta;
+            fe9_from_const(beta, BETA);
+            fe9_mul(P.x, P.x, beta);
+        }
+#endif
+        fe9_neg<1>(P.y, T[0].y);
+        fe9_cmov(P.y, T[0].y, ng);
+        gej9 tmp;
         bool tinf = ainf;
-        gej_add_ge(tmp, tinf, acc, P);
+        gej9_add_ge(tmp, tinf, acc, P);
         if (sk) {
             acc = tmp;
             ainf = tinf;
         }
     }
-    fe_mul(acc.z, acc.z, zfac);  // back from E'' to E
+    fe9_mul(acc.z, acc.z, zfac);  // back from E'' to E (2*1 -> 1)
 
     // ---- u1 * G via comb
-    gej accg;
+    gej9 accg;
     bool ginf;
-    comb_mul_g(accg, ginf, u1, gtab);
+    comb_mul_g9(accg, ginf, u1, gtab);
 
     // ---- Q = u2 R + u1 G
-    gej q;
+    gej9 q;
     bool qinf;
-    gej_add(q, qinf, acc, ainf, accg, ginf);
+    gej9_add(q, qinf, acc, ainf, accg, ginf);
     ok = ok && !qinf;
-
-    fe zi, zi2;
-    fe_inv(zi, q.z);
-    fe_sqr(zi2, zi);
-    fe_mul(qx, q.x, zi2);
-    fe_mul(zi2, zi2, zi);
-    fe_mul(qy, q.y, zi2);
+    gej9_to_affine_words(qx, qy, q);
     return ok ? GSV_ST_OK : GSV_ST_RECOVER_FAILED;
 }
 
@@ -433,24 +451,15 @@ GSV_DI void ecdsa_sign(uint32_t r_out[8], uint32_t s_out[8], uint32_t& recid, fe
     if (sc_is_zero(k)) k.v[0] = 1;
     sc mr;
     sc_cond_sub_n(mr.v, m, 0);
-    gej P;
+    gej9 P;
     bool pinf;
-    comb_mul_g(P, pinf, d, gtab);
-    fe zi, zi2;
-    fe_inv(zi, P.z);
-    fe_sqr(zi2, zi);
-    fe_mul(px, P.x, zi2);
-    fe_mul(zi2, zi2, zi);
-    fe_mul(py, P.y, zi2);
-    gej R;
+    comb_mul_g9(P, pinf, d, gtab);
+    gej9_to_affine_words(px, py, P);
+    gej9 R;
     bool rinf;
-    comb_mul_g(R, rinf, k, gtab);
+    comb_mul_g9(R, rinf, k, gtab);
     fe rx, ry;
-    fe_inv(zi, R.z);
-    fe_sqr(zi2, zi);
-    fe_mul(rx, R.x, zi2);
-    fe_mul(zi2, zi2, zi);
-    fe_mul(ry, R.y, zi2);
+    gej9_to_affine_words(rx, ry, R);
     recid = ry.v[0] & 1u;
     sc r;
     bool over = !limbs_lt(rx.v, SN);

@@ -102,14 +102,27 @@ GSV_DI void fe_reduce(fe& r, const uint32_t t[16]) {
     fe_cond_sub_p(r.v, s, 0);
 }
 
+// GSV_FE_FX=1: whole-product asm statements (mul_8x8_fx / sqr_8_fx, dedicated squaring);
+// 0: the per-column statements (A/B timing only)
+#ifndef GSV_FE_FX
+#define GSV_FE_FX 1
+#endif
 GSV_DI void fe_mul(fe& r, const fe& a, const fe& b) {
     uint32_t t[16];
+#if GSV_FE_FX
+    mul_8x8_fx(t, a.v, b.v);
+#else
     mul_8x8_asm(t, a.v, b.v);
+#endif
     fe_reduce(r, t);
 }
 GSV_DI void fe_sqr(fe& r, const fe& a) {
     uint32_t t[16];
+#if GSV_FE_FX
+    sqr_8_fx(t, a.v);
+#else
     mul_8x8_asm(t, a.v, a.v);
+#endif
     fe_reduce(r, t);
 }
 GSV_DI void fe_sqr_n(fe& r, const fe& a, int n) {
@@ -276,7 +289,7 @@ GSV_DI void sc_reduce(sc& r, const uint32_t t[16]) {
     const uint32_t C4[4] = {SNC[0], SNC[1], SNC[2], SNC[3]};
     // stage 1: m = L + H*SNC' + H*2^128  (< 2^386, 13 limbs)
     uint32_t p[12], m[13], c = 0;
-    mul_8x4_asm(p, t + 8, C4);
+    mul_8x4_fx(p, t + 8, C4);
 #pragma unroll
     for (int i = 0; i < 8; i++) m[i] = addc(t[i], p[i], c);
 #pragma unroll
@@ -288,7 +301,7 @@ GSV_DI void sc_reduce(sc& r, const uint32_t t[16]) {
     m[12] += c;
     // stage 2: m2 = m[0..7] + m[8..12]*SNC' + m[8..12]*2^128  (< 2^291, 10 limbs)
     uint32_t p2[9], m2[10];
-    mul_5x4_asm(p2, m + 8, C4);
+    mul_5x4_fx(p2, m + 8, C4);
     c = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) m2[i] = addc(m[i], p2[i], c);
@@ -300,7 +313,7 @@ GSV_DI void sc_reduce(sc& r, const uint32_t t[16]) {
     m2[9] += c;
     // stage 3: m3 = m2[0..7] + m2[8..9]*SNC' + m2[8..9]*2^128  (< 2^256 + 2^166, carry limb 0/1)
     uint32_t p3[6], m3[8];
-    mul_2x4_asm(p3, m2 + 8, C4);
+    mul_2x4_fx(p3, m2 + 8, C4);
     c = 0;
 #pragma unroll
     for (int i = 0; i < 6; i++) m3[i] = addc(m2[i], p3[i], c);
@@ -317,12 +330,12 @@ GSV_DI void sc_reduce(sc& r, const uint32_t t[16]) {
 
 GSV_DI void sc_mul(sc& r, const sc& a, const sc& b) {
     uint32_t t[16];
-    mul_8x8_asm(t, a.v, b.v);
+    mul_8x8_fx(t, a.v, b.v);
     sc_reduce(r, t);
 }
 GSV_DI void sc_sqr(sc& r, const sc& a) {
     uint32_t t[16];
-    mul_8x8_asm(t, a.v, a.v);
+    sqr_8_fx(t, a.v);
     sc_reduce(r, t);
 }
 GSV_DI bool sc_is_zero(const sc& a) {
