@@ -8,6 +8,7 @@
 namespace gsv { struct gej9; __device__ void gej9_dbl_rare(gej9& o, const gej9& p); }
 #define GEJ9_DBL_RARE(o, p) gej9_dbl_rare(o, p)
 #include "secp256k1_fe9.cuh"
+#include "modinv30.cuh"
 
 namespace gsv {
 
@@ -225,7 +226,14 @@ GSV_DI void comb_mul_g9(gej9& acc, bool& inf, const sc& u, const uint4* __restri
 // Jacobian -> affine canonical 8 x 32-bit words
 GSV_DI void gej9_to_affine_words(fe& ax, fe& ay, const gej9& q) {
     fe9 zi, zi2, x, y;
-    fe9_inv(zi, q.z);
+    {
+        fe9 z = q.z;
+        fe9_normalize_full(z);
+        uint32_t zw[8], iw[8];
+        fe9_to_words(zw, z);
+        modinv30_words(iw, zw, MI30_P);  // Z^-1 mod p (safegcd)
+        fe9_from_words(zi, iw);
+    }
     fe9_sqr(zi2, zi);
     fe9_mul(x, q.x, zi2);
     fe9_mul(zi2, zi2, zi);
@@ -280,7 +288,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     }
     // u1 = -m / r, u2 = s / r
     sc rn, u1, u2;
-    sc_inv(rn, rs);
+    modinv30_words(rn.v, rs.v, MI30_N);  // r^-1 mod n (safegcd; r != 0 on every valid path)
     sc_mul(u1, rn, m);
     sc_neg(u1, u1);
     sc_mul(u2, rn, ss);
@@ -467,7 +475,7 @@ GSV_DI void ecdsa_sign(uint32_t r_out[8], uint32_t s_out[8], uint32_t& recid, fe
     if (over) recid |= 2u;
     // s = k^-1 (m + r d)
     sc kinv, s, t;
-    sc_inv(kinv, k);
+    modinv30_words(kinv.v, k.v, MI30_N);
     sc_mul(t, r, d);
     sc_add(t, t, mr);
     sc_mul(s, kinv, t);

@@ -268,3 +268,20 @@ def test_build_r_table(lib):
             tx, ty = val(T[18 * e:18 * e + 9]) % P, val(T[18 * e + 9:18 * e + 18]) % P
             zi = inv(zf)
             assert (tx * zi * zi % P, ty * zi * zi * zi % P) == mul_pt(2 * e + 1, R)
+
+
+N_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+def test_safegcd_modinv(lib):
+    """modinv30.cuh (Bernstein-Yang divsteps) against pow(x, -1, m) for m = n and m = p."""
+    rng = random.Random(20)
+    W8 = ctypes.c_uint32 * 8
+    for which, m in ((0, N_ORDER), (1, P)):
+        xs = [0, 1, 2, 3, m - 1, m - 2, (m - 1) // 2, 2**255, 2**128 + 1, 0xFFFFFFFF] + [rng.randrange(1, m) for _ in range(3000)]
+        xs += [rng.getrandbits(rng.randrange(1, 256)) % m for _ in range(500)]
+        for x in xs:
+            out = W8()
+            lib.h_modinv(out, W8(*[(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)]), which)
+            got = sum(v << (32 * i) for i, v in enumerate(out))
+            assert got == (pow(x, -1, m) if x else 0), (which, hex(x), hex(got))

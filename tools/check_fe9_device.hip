@@ -35,6 +35,10 @@ __global__ void k_ops(const uint32_t* in, uint32_t* out, int n) {
     gsv::fe9 a2; gsv::fe9_add(a2, a, a); gsv::fe9_sqr(t, a2); for (int k = 0; k < 9; k++) o2[18 + k] = t.v[k];  // sqr mag2
     gsv::fe9_sqr_n(t, a, 3); for (int k = 0; k < 9; k++) o2[27 + k] = t.v[k];                            // sqr_n loop
     gsv::fe9_mul(t, a, b); gsv::fe9_mul(t, t, b); for (int k = 0; k < 9; k++) o2[36 + k] = t.v[k];       // mul(mul)
+    uint32_t* o3 = out + (size_t)n * 135 + (size_t)i * 16;
+    uint32_t aw[8], iw[8]; gsv::fe9 an = a; gsv::fe9_normalize_full(an); gsv::fe9_to_words(aw, an);
+    gsv::modinv30_words(iw, aw, gsv::MI30_P); for (int k = 0; k < 8; k++) o3[k] = iw[k];
+    gsv::modinv30_words(iw, aw, gsv::MI30_N); for (int k = 0; k < 8; k++) o3[8 + k] = iw[k];
 }
 
 __global__ void k_recover(const uint8_t* msg, const uint8_t* sig, const uint4* gtab, uint32_t* out) {
@@ -56,11 +60,11 @@ int main() {
     for (int i = 0; i < n; i++) { h[i * 18 + 8] &= 0xFFFFFF; h[i * 18 + 17] &= 0xFFFFFF; }
     uint32_t *din, *dout;
     CHECK(hipMalloc(&din, h.size() * 4));
-    CHECK(hipMalloc(&dout, (size_t)n * 135 * 4));
+    CHECK(hipMalloc(&dout, (size_t)n * 151 * 4));
     CHECK(hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_ops, dim3(n / 64), dim3(64), 0, 0, din, dout, n);
     CHECK(hipDeviceSynchronize());
-    std::vector<uint32_t> o((size_t)n * 135);
+    std::vector<uint32_t> o((size_t)n * 151);
     CHECK(hipMemcpy(o.data(), dout, o.size() * 4, hipMemcpyDeviceToHost));
     FILE* f = fopen("gpurun_out/fe9_dev_in.bin", "wb"); fwrite(h.data(), 4, h.size(), f); fclose(f);
     f = fopen("gpurun_out/fe9_dev_out.bin", "wb"); fwrite(o.data(), 4, o.size(), f); fclose(f);
