@@ -25,9 +25,9 @@ namespace gsv {
 
 // ---------------------------------------------------------------------------- kernels
 #ifndef GSV_ECR_WAVES
-#define GSV_ECR_WAVES 2
+#define GSV_ECR_WAVES 3
 #endif
-// ~258 live VGPRs: 2 waves/SIMD with a couple of spilled registers beats 1 wave/SIMD spill-free
+// 3 waves/SIMD (<= 168 VGPRs): the GLV table sits in per-lane scratch (recover_dev.cuh)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAVES, GSV_ECR_WAVES))) void k_ecrecover(const uint8_t* __restrict__ msg32,
                                                    const uint8_t* __restrict__ sig65, uint32_t n,
                                                    const uint4* __restrict__ gtab,

@@ -236,7 +236,7 @@ GSV_DI void keccak_stream(uint64_t a[25], const PreStream& s) {
     }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_notary_tx(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_notary_tx(
     const uint8_t* __restrict__ bodies, const uint64_t* __restrict__ body_off, const BlobRec* __restrict__ blobs,
     const uint32_t* __restrict__ ntx, uint32_t max_txs, const uint8_t* __restrict__ cid64,
     const uint8_t* __restrict__ suffix, uint32_t slen, int signer_kind, const uint4* __restrict__ gtab,

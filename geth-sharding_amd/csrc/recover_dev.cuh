@@ -33,10 +33,9 @@ __device__ constexpr uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75F
 __device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
                                            0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
 
-// GSV_LX_TABLE=1 keeps the four lambda-table x-coordinates (beta * x) in registers (36 VGPRs);
-// 0 recomputes beta * x per lambda add (+44 field products, no spills at 2 waves/SIMD)
-#ifndef GSV_LX_TABLE
-#define GSV_LX_TABLE 0
+// GSV_GLV_PREFETCH=1 loads a digit's two table entries before its doublings
+#ifndef GSV_GLV_PREFETCH
+#define GSV_GLV_PREFETCH 0
 #endif
 constexpr int GLV_DIGITS = 44;  // w = 3 odd digits cover k < 2^131 (bound is 2^128)
 
@@ -313,21 +312,72 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     ge9 T[4];
     fe9 zfac;
     build_r_table9(T, zfac, x, y);
-#if GSV_LX_TABLE
-    fe9 LX[4];
+    // The table lives in per-lane private memory (scratch: swizzled per lane, so a wave's loads
+    // coalesce), not in VGPRs: 108 words {x[4], y[4], beta*x[4]} would otherwise hold the kernel
+    // at 2 waves/SIMD, and one wave alone issues a heavy VALU op only every ~8.7 cycles
+    // (profiles/r01_microbench_lat.txt).  Each add loads its entry by index (no selects).
+    uint32_t tm[108];
     {
-        fe9 beta;
+        fe9 beta, lx;
         fe9_from_const(beta, BETA);
 #pragma unroll
-        for (int e = 0; e < 4; e++) fe9_mul(LX[e], T[e].x, beta);
+        for (int e = 0; e < 4; e++) {
+            fe9_mul(lx, T[e].x, beta);
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                tm[e * 9 + k] = T[e].x.v[k];
+                tm[36 + e * 9 + k] = T[e].y.v[k];
+                tm[72 + e * 9 + k] = lx.v[k];
+            }
+        }
     }
-#endif
 
     gej9 acc;
     bool ainf = true;
     acc.x = T[0].x;
     acc.y = T[0].y;
     fe9_set_u32(acc.z, 1);
+#if GSV_GLV_PREFETCH
+    // entries of digit i are loaded before its three doublings (~30k cycles ahead of their use)
+    ge9 Q1, Q2;
+    uint32_t c1n = (dig1[(GLV_DIGITS - 1) >> 3] >> (((GLV_DIGITS - 1) & 7) * 4)) & 15u;
+    uint32_t c2n = (dig2[(GLV_DIGITS - 1) >> 3] >> (((GLV_DIGITS - 1) & 7) * 4)) & 15u;
+#pragma unroll 1
+    for (int i = GLV_DIGITS - 1; i >= 0; i--) {
+        uint32_t c1 = c1n, c2 = c2n;
+        {
+            uint32_t x1 = (c1 & 3u) * 9u, x2 = 72u + (c2 & 3u) * 9u;
+            uint32_t y1 = 36u + (c1 & 3u) * 9u, y2 = 36u + (c2 & 3u) * 9u;
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                Q1.x.v[k] = tm[x1 + k];
+                Q1.y.v[k] = tm[y1 + k];
+                Q2.x.v[k] = tm[x2 + k];
+                Q2.y.v[k] = tm[y2 + k];
+            }
+        }
+        if (i > 0) {
+            c1n = (sel_word(dig1, (uint32_t)(i - 1) >> 3) >> (((i - 1) & 7) * 4)) & 15u;
+            c2n = (sel_word(dig2, (uint32_t)(i - 1) >> 3) >> (((i - 1) & 7) * 4)) & 15u;
+        }
+        if (i != GLV_DIGITS - 1) {
+#pragma unroll 1
+            for (int d = 0; d < 3; d++) gej9_dbl(acc, acc);
+        }
+        // one add body, two passes: digit of k1 on T, digit of k2 on lambda(T) = (beta x, y)
+#pragma unroll 1
+        for (int j = 0; j < 2; j++) {
+            uint32_t c = j ? c2 : c1;
+            bool ng = j ? neg2 : neg1;
+            ge9 P = Q1;
+            ge9_cmov(P, Q2, j != 0);
+            fe9 ny;
+            fe9_neg<1>(ny, P.y);         // 2
+            fe9_cmov(P.y, ny, ((c >> 3) != 0) != ng);
+            gej9_add_ge(acc, ainf, acc, P);
+        }
+    }
+#else
 #pragma unroll 1
     for (int i = GLV_DIGITS - 1; i >= 0; i--) {
         if (i != GLV_DIGITS - 1) {
@@ -336,48 +386,39 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         }
         uint32_t c1 = (sel_word(dig1, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
         uint32_t c2 = (sel_word(dig2, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
-        // one add body, two passes: digit of k1 on T, digit of k2 on lambda(T)
+        // one add body, two passes: digit of k1 on T, digit of k2 on lambda(T) = (beta x, y)
 #pragma unroll 1
         for (int j = 0; j < 2; j++) {
             uint32_t c = j ? c2 : c1;
             bool ng = j ? neg2 : neg1;
+            uint32_t xo = (j ? 72u : 0u) + (c & 3u) * 9u, yo = 36u + (c & 3u) * 9u;
             ge9 P;
-            table_select9(P, T, c & 3u);
-#if GSV_LX_TABLE
-            fe9 lx;
-            table_select9_x(lx, LX, c & 3u);
-            fe9_cmov(P.x, lx, j != 0);
-#else
-            if (j != 0) {  // lambda(x, y) = (beta x, y); wave-uniform branch
-                fe9 beta;
-                fe9_from_const(beta, BETA);
-                fe9_mul(P.x, P.x, beta);
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                P.x.v[k] = tm[xo + k];
+                P.y.v[k] = tm[yo + k];
             }
-#endif
             fe9 ny;
             fe9_neg<1>(ny, P.y);         // 2
             fe9_cmov(P.y, ny, ((c >> 3) != 0) != ng);
             gej9_add_ge(acc, ainf, acc, P);
         }
     }
+#endif
     // skew corrections: the recoded scalars were k + skew -> subtract (+-)T0 / (+-)lambda(T0)
 #pragma unroll 1
     for (int j = 0; j < 2; j++) {
         bool ng = j ? neg2 : neg1;
         uint32_t sk = j ? skew2 : skew1;
         ge9 P;
-        P.x = T[0].x;
-#if GSV_LX_TABLE
-        fe9_cmov(P.x, LX[0], j != 0);
-#else
-        if (j != 0) {
-            fe9 beta;
-            fe9_from_const(beta, BETA);
-            fe9_mul(P.x, P.x, beta);
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            P.x.v[k] = tm[(j ? 72 : 0) + k];
+            P.y.v[k] = tm[36 + k];
         }
-#endif
-        fe9_neg<1>(P.y, T[0].y);
-        fe9_cmov(P.y, T[0].y, ng);
+        fe9 ny;
+        fe9_neg<1>(ny, P.y);
+        fe9_cmov(P.y, ny, !ng);
         gej9 tmp;
         bool tinf = ainf;
         gej9_add_ge(tmp, tinf, acc, P);
