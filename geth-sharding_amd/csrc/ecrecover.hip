@@ -25,15 +25,16 @@ namespace gsv {
 
 // ---------------------------------------------------------------------------- kernels
 #ifndef GSV_ECR_WAVES
-#define GSV_ECR_WAVES 3
+#define GSV_ECR_WAVES 2
 #endif
-// 3 waves/SIMD (<= 168 VGPRs): the GLV table sits in per-lane scratch (recover_dev.cuh)
+// 2 waves/SIMD: two 256-thread blocks per CU share its 160 KiB LDS (72 KiB GLV table each)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAVES, GSV_ECR_WAVES))) void k_ecrecover(const uint8_t* __restrict__ msg32,
                                                    const uint8_t* __restrict__ sig65, uint32_t n,
                                                    const uint4* __restrict__ gtab,
                                                    uint8_t* __restrict__ pub65,
                                                    uint8_t* __restrict__ addr20,
                                                    uint8_t* __restrict__ status) {
+    __shared__ uint32_t ltab[GSV_LTAB_WORDS];
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t* sg = sig65 + (size_t)i * 65;
@@ -43,7 +44,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     load32_be(s, sg + 32);
     uint32_t recid = sg[64];
     fe qx, qy;
-    uint32_t st = recover_core(qx, qy, msg, r, s, recid & 3u, gtab);
+    uint32_t st = recover_core(qx, qy, msg, r, s, recid & 3u, gtab, ltab + threadIdx.x);
     if (recid >= 4) st = GSV_ST_INVALID_RECID;
     bool ok = st == GSV_ST_OK;
     store_pub_addr(pub65 ? pub65 + (size_t)i * 65 : nullptr, addr20 ? addr20 + (size_t)i * 20 : nullptr,
@@ -61,6 +62,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
                                                 int homestead, const uint4* __restrict__ gtab,
                                                 uint8_t* __restrict__ addr20,
                                                 uint8_t* __restrict__ status) {
+    __shared__ uint32_t ltab[GSV_LTAB_WORDS];
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t msg[8], r[8], s[8];
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     valid = valid && !(homestead && limbs_lt(HALF_N, s));
     valid = valid && limbs_lt(r, SN) && limbs_lt(s, SN) && (V == 0 || V == 1);
     fe qx, qy;
-    uint32_t st = recover_core(qx, qy, msg, r, s, V & 1u, gtab);
+    uint32_t st = recover_core(qx, qy, msg, r, s, V & 1u, gtab, ltab + threadIdx.x);
     if (!valid) st = GSV_ST_INVALID_SIG;
     store_pub_addr(nullptr, addr20 + (size_t)i * 20, st == GSV_ST_OK, qx, qy);
     status[i] = (uint8_t)st;

@@ -33,10 +33,10 @@ __device__ constexpr uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75F
 __device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
                                            0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
 
-// GSV_GLV_PREFETCH=1 loads a digit's two table entries before its doublings
-#ifndef GSV_GLV_PREFETCH
-#define GSV_GLV_PREFETCH 0
-#endif
+// LDS table: 72 words per lane, lane-minor ([word][GSV_LTAB_STRIDE]); the kernels that call
+// recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS]
+constexpr int GSV_LTAB_STRIDE = 256;
+constexpr int GSV_LTAB_WORDS = 72 * GSV_LTAB_STRIDE;
 constexpr int GLV_DIGITS = 44;  // w = 3 odd digits cover k < 2^131 (bound is 2^128)
 
 // ---------------------------------------------------------------------------- scalar helpers
@@ -247,7 +247,8 @@ GSV_DI void gej9_to_affine_words(fe& ax, fe& ay, const gej9& q) {
 // Returns GSV_ST_OK or GSV_ST_RECOVER_FAILED; on OK (qx, qy) is the affine public key.
 // msg/r/s are 256-bit values as little-endian limbs; recid in 0..3.
 GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32_t r[8],
-                             const uint32_t s[8], uint32_t recid, const uint4* __restrict__ gtab) {
+                             const uint32_t s[8], uint32_t recid, const uint4* __restrict__ gtab,
+                             uint32_t* __restrict__ ltab) {
     bool ok = limbs_lt(r, SN) && limbs_lt(s, SN);
     sc rs, ss, m;
 #pragma unroll
@@ -312,23 +313,16 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     ge9 T[4];
     fe9 zfac;
     build_r_table9(T, zfac, x, y);
-    // The table lives in per-lane private memory (scratch: swizzled per lane, so a wave's loads
-    // coalesce), not in VGPRs: 108 words {x[4], y[4], beta*x[4]} would otherwise hold the kernel
-    // at 2 waves/SIMD, and one wave alone issues a heavy VALU op only every ~8.7 cycles
-    // (profiles/r01_microbench_lat.txt).  Each add loads its entry by index (no selects).
-    uint32_t tm[108];
-    {
-        fe9 beta, lx;
-        fe9_from_const(beta, BETA);
+    // The GLV table lives in LDS (ltab = this lane's column of a [word][256 lanes] array:
+    // conflict-free for any per-lane entry index), not in VGPRs: 72 words {x[4], y[4]} would
+    // otherwise cost the kernel occupancy.  Each add loads its entry by index (no selects);
+    // lambda(P) = (beta x, y) costs one product per lambda add.
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            fe9_mul(lx, T[e].x, beta);
+    for (int e = 0; e < 4; e++) {
 #pragma unroll
-            for (int k = 0; k < 9; k++) {
-                tm[e * 9 + k] = T[e].x.v[k];
-                tm[36 + e * 9 + k] = T[e].y.v[k];
-                tm[72 + e * 9 + k] = lx.v[k];
-            }
+        for (int k = 0; k < 9; k++) {
+            ltab[(e * 9 + k) * GSV_LTAB_STRIDE] = T[e].x.v[k];
+            ltab[(36 + e * 9 + k) * GSV_LTAB_STRIDE] = T[e].y.v[k];
         }
     }
 
@@ -337,47 +331,6 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     acc.x = T[0].x;
     acc.y = T[0].y;
     fe9_set_u32(acc.z, 1);
-#if GSV_GLV_PREFETCH
-    // entries of digit i are loaded before its three doublings (~30k cycles ahead of their use)
-    ge9 Q1, Q2;
-    uint32_t c1n = (dig1[(GLV_DIGITS - 1) >> 3] >> (((GLV_DIGITS - 1) & 7) * 4)) & 15u;
-    uint32_t c2n = (dig2[(GLV_DIGITS - 1) >> 3] >> (((GLV_DIGITS - 1) & 7) * 4)) & 15u;
-#pragma unroll 1
-    for (int i = GLV_DIGITS - 1; i >= 0; i--) {
-        uint32_t c1 = c1n, c2 = c2n;
-        {
-            uint32_t x1 = (c1 & 3u) * 9u, x2 = 72u + (c2 & 3u) * 9u;
-            uint32_t y1 = 36u + (c1 & 3u) * 9u, y2 = 36u + (c2 & 3u) * 9u;
-#pragma unroll
-            for (int k = 0; k < 9; k++) {
-                Q1.x.v[k] = tm[x1 + k];
-                Q1.y.v[k] = tm[y1 + k];
-                Q2.x.v[k] = tm[x2 + k];
-                Q2.y.v[k] = tm[y2 + k];
-            }
-        }
-        if (i > 0) {
-            c1n = (sel_word(dig1, (uint32_t)(i - 1) >> 3) >> (((i - 1) & 7) * 4)) & 15u;
-            c2n = (sel_word(dig2, (uint32_t)(i - 1) >> 3) >> (((i - 1) & 7) * 4)) & 15u;
-        }
-        if (i != GLV_DIGITS - 1) {
-#pragma unroll 1
-            for (int d = 0; d < 3; d++) gej9_dbl(acc, acc);
-        }
-        // one add body, two passes: digit of k1 on T, digit of k2 on lambda(T) = (beta x, y)
-#pragma unroll 1
-        for (int j = 0; j < 2; j++) {
-            uint32_t c = j ? c2 : c1;
-            bool ng = j ? neg2 : neg1;
-            ge9 P = Q1;
-            ge9_cmov(P, Q2, j != 0);
-            fe9 ny;
-            fe9_neg<1>(ny, P.y);         // 2
-            fe9_cmov(P.y, ny, ((c >> 3) != 0) != ng);
-            gej9_add_ge(acc, ainf, acc, P);
-        }
-    }
-#else
 #pragma unroll 1
     for (int i = GLV_DIGITS - 1; i >= 0; i--) {
         if (i != GLV_DIGITS - 1) {
@@ -391,12 +344,17 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         for (int j = 0; j < 2; j++) {
             uint32_t c = j ? c2 : c1;
             bool ng = j ? neg2 : neg1;
-            uint32_t xo = (j ? 72u : 0u) + (c & 3u) * 9u, yo = 36u + (c & 3u) * 9u;
+            uint32_t xo = (c & 3u) * 9u;
             ge9 P;
 #pragma unroll
             for (int k = 0; k < 9; k++) {
-                P.x.v[k] = tm[xo + k];
-                P.y.v[k] = tm[yo + k];
+                P.x.v[k] = ltab[(xo + k) * GSV_LTAB_STRIDE];
+                P.y.v[k] = ltab[(36u + xo + k) * GSV_LTAB_STRIDE];
+            }
+            if (j != 0) {  // wave-uniform
+                fe9 beta;
+                fe9_from_const(beta, BETA);
+                fe9_mul(P.x, P.x, beta);
             }
             fe9 ny;
             fe9_neg<1>(ny, P.y);         // 2
@@ -404,17 +362,18 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             gej9_add_ge(acc, ainf, acc, P);
         }
     }
-#endif
     // skew corrections: the recoded scalars were k + skew -> subtract (+-)T0 / (+-)lambda(T0)
 #pragma unroll 1
     for (int j = 0; j < 2; j++) {
         bool ng = j ? neg2 : neg1;
         uint32_t sk = j ? skew2 : skew1;
         ge9 P;
-#pragma unroll
-        for (int k = 0; k < 9; k++) {
-            P.x.v[k] = tm[(j ? 72 : 0) + k];
-            P.y.v[k] = tm[36 + k];
+        P.x = T[0].x;
+        P.y = T[0].y;
+        if (j != 0) {
+            fe9 beta;
+            fe9_from_const(beta, BETA);
+            fe9_mul(P.x, P.x, beta);
         }
         fe9 ny;
         fe9_neg<1>(ny, P.y);
