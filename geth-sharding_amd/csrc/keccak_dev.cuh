@@ -1,6 +1,7 @@
 // Keccak-f[1600] and Keccak-256 (pre-FIPS padding 0x01 ... 0x80, rate 136) on gfx950 VALU.
-// One message per lane; the 25 x 64-bit state lives in 50 VGPRs.  64-bit rotates lower to
-// v_alignbit_b32 pairs, theta's 5-way XORs and chi's a ^ (~b & c) to v_bitop3_b32.
+// One message per lane; the 25 x 64-bit state lives in 50 VGPRs as 32-bit halves.  64-bit rotates
+// are explicit v_alignbit_b32 pairs, theta's 5-way XORs and chi's a ^ (~b & c) explicit v_bitop3_b32
+// (the compiler's own lowering of the uint64 form was 64-bit shifts + v_bfi + v_xor: ~20% more issue).
 // Restates crypto/sha3/keccakf.go:39 (permutation), :10 (round constants) and
 // crypto/sha3/sha3.go:98-157 + hashes.go:16 (sponge, rate 136, dsbyte 0x01).
 #pragma once
@@ -19,85 +20,89 @@ __device__ constexpr uint64_t KECCAK_RC[24] = {
     0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
     0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
 
+// v_bitop3_b32 truth tables (index = S0<<2 | S1<<1 | S2): S0^S1^S2, and chi's S0 ^ (~S1 & S2)
+#ifndef GSV_BITOP3_CHI
+#define GSV_BITOP3_CHI 0xD2
+#endif
+constexpr uint32_t BITOP3_XOR3 = 0x96;
+
+GSV_DI uint32_t kxor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, BITOP3_XOR3); }
+GSV_DI uint32_t kchi(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, GSV_BITOP3_CHI); }
+
+// 64-bit rotate-left by R of (hi:lo): two v_alignbit_b32 (rotates by 0/32 are register renames)
 template <int R>
-GSV_DI uint64_t rotl64(uint64_t x) {
-    if constexpr (R == 0) return x;
-    else return (x << R) | (x >> (64 - R));
+GSV_DI void krot(uint32_t& olo, uint32_t& ohi, uint32_t lo, uint32_t hi) {
+    if constexpr (R == 0) {
+        olo = lo;
+        ohi = hi;
+    } else if constexpr (R < 32) {
+        ohi = __builtin_amdgcn_alignbit(hi, lo, 32 - R);
+        olo = __builtin_amdgcn_alignbit(lo, hi, 32 - R);
+    } else if constexpr (R == 32) {
+        olo = hi;
+        ohi = lo;
+    } else {
+        ohi = __builtin_amdgcn_alignbit(lo, hi, 64 - R);
+        olo = __builtin_amdgcn_alignbit(hi, lo, 64 - R);
+    }
 }
 
-GSV_DI uint64_t xor5(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e) {
-    return a ^ b ^ c ^ d ^ e;
+// rho offsets r[x + 5y] (crypto/sha3/keccakf.go) and pi destinations: b[y + 5((2x + 3y) mod 5)]
+__device__ constexpr int KECCAK_RHO[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
+                                           25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
+
+template <int I>
+GSV_DI void theta_rho_pi(uint32_t bl[25], uint32_t bh[25], const uint32_t al[25], const uint32_t ah[25],
+                         const uint32_t dl[5], const uint32_t dh[5]) {
+    constexpr int x = I % 5, y = I / 5;
+    constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
+    krot<KECCAK_RHO[I]>(bl[dst], bh[dst], al[I] ^ dl[x], ah[I] ^ dh[x]);
+    if constexpr (I + 1 < 25) theta_rho_pi<I + 1>(bl, bh, al, ah, dl, dh);
 }
 
-// One full permutation, rounds fully unrolled in-place (lane index x + 5y).
-GSV_DI void keccakf(uint64_t a[25]) {
+// One full permutation over the state split into 32-bit halves (lane index x + 5y).  Per round:
+// theta's column parities as 20 three-way v_bitop3, rho as 48 v_alignbit, chi as 50 v_bitop3.
+GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) {
 #pragma unroll 1
     for (int round = 0; round < 24; round++) {
-        uint64_t c0 = xor5(a[0], a[5], a[10], a[15], a[20]);
-        uint64_t c1 = xor5(a[1], a[6], a[11], a[16], a[21]);
-        uint64_t c2 = xor5(a[2], a[7], a[12], a[17], a[22]);
-        uint64_t c3 = xor5(a[3], a[8], a[13], a[18], a[23]);
-        uint64_t c4 = xor5(a[4], a[9], a[14], a[19], a[24]);
-        uint64_t d0 = c4 ^ rotl64<1>(c1);
-        uint64_t d1 = c0 ^ rotl64<1>(c2);
-        uint64_t d2 = c1 ^ rotl64<1>(c3);
-        uint64_t d3 = c2 ^ rotl64<1>(c4);
-        uint64_t d4 = c3 ^ rotl64<1>(c0);
-        // theta + rho + pi: b[y][2x+3y] = rot(a[x][y] ^ d[x], r[x][y])
-        uint64_t b0 = a[0] ^ d0;
-        uint64_t b10 = rotl64<1>(a[1] ^ d1);
-        uint64_t b20 = rotl64<62>(a[2] ^ d2);
-        uint64_t b5 = rotl64<28>(a[3] ^ d3);
-        uint64_t b15 = rotl64<27>(a[4] ^ d4);
-        uint64_t b16 = rotl64<36>(a[5] ^ d0);
-        uint64_t b1 = rotl64<44>(a[6] ^ d1);
-        uint64_t b11 = rotl64<6>(a[7] ^ d2);
-        uint64_t b21 = rotl64<55>(a[8] ^ d3);
-        uint64_t b6 = rotl64<20>(a[9] ^ d4);
-        uint64_t b7 = rotl64<3>(a[10] ^ d0);
-        uint64_t b17 = rotl64<10>(a[11] ^ d1);
-        uint64_t b2 = rotl64<43>(a[12] ^ d2);
-        uint64_t b12 = rotl64<25>(a[13] ^ d3);
-        uint64_t b22 = rotl64<39>(a[14] ^ d4);
-        uint64_t b23 = rotl64<41>(a[15] ^ d0);
-        uint64_t b8 = rotl64<45>(a[16] ^ d1);
-        uint64_t b18 = rotl64<15>(a[17] ^ d2);
-        uint64_t b3 = rotl64<21>(a[18] ^ d3);
-        uint64_t b13 = rotl64<8>(a[19] ^ d4);
-        uint64_t b14 = rotl64<18>(a[20] ^ d0);
-        uint64_t b24 = rotl64<2>(a[21] ^ d1);
-        uint64_t b9 = rotl64<61>(a[22] ^ d2);
-        uint64_t b19 = rotl64<56>(a[23] ^ d3);
-        uint64_t b4 = rotl64<14>(a[24] ^ d4);
-        // chi
-        a[0] = b0 ^ (~b1 & b2);
-        a[1] = b1 ^ (~b2 & b3);
-        a[2] = b2 ^ (~b3 & b4);
-        a[3] = b3 ^ (~b4 & b0);
-        a[4] = b4 ^ (~b0 & b1);
-        a[5] = b5 ^ (~b6 & b7);
-        a[6] = b6 ^ (~b7 & b8);
-        a[7] = b7 ^ (~b8 & b9);
-        a[8] = b8 ^ (~b9 & b5);
-        a[9] = b9 ^ (~b5 & b6);
-        a[10] = b10 ^ (~b11 & b12);
-        a[11] = b11 ^ (~b12 & b13);
-        a[12] = b12 ^ (~b13 & b14);
-        a[13] = b13 ^ (~b14 & b10);
-        a[14] = b14 ^ (~b10 & b11);
-        a[15] = b15 ^ (~b16 & b17);
-        a[16] = b16 ^ (~b17 & b18);
-        a[17] = b17 ^ (~b18 & b19);
-        a[18] = b18 ^ (~b19 & b15);
-        a[19] = b19 ^ (~b15 & b16);
-        a[20] = b20 ^ (~b21 & b22);
-        a[21] = b21 ^ (~b22 & b23);
-        a[22] = b22 ^ (~b23 & b24);
-        a[23] = b23 ^ (~b24 & b20);
-        a[24] = b24 ^ (~b20 & b21);
-        // iota
-        a[0] ^= KECCAK_RC[round];
+        uint32_t cl[5], ch[5], dl[5], dh[5];
+#pragma unroll
+        for (int x = 0; x < 5; x++) {
+            cl[x] = kxor3(kxor3(al[x], al[x + 5], al[x + 10]), al[x + 15], al[x + 20]);
+            ch[x] = kxor3(kxor3(ah[x], ah[x + 5], ah[x + 10]), ah[x + 15], ah[x + 20]);
+        }
+#pragma unroll
+        for (int x = 0; x < 5; x++) {
+            uint32_t rl, rh;
+            krot<1>(rl, rh, cl[(x + 1) % 5], ch[(x + 1) % 5]);
+            dl[x] = cl[(x + 4) % 5] ^ rl;
+            dh[x] = ch[(x + 4) % 5] ^ rh;
+        }
+        uint32_t bl[25], bh[25];
+        theta_rho_pi<0>(bl, bh, al, ah, dl, dh);
+#pragma unroll
+        for (int y = 0; y < 25; y += 5) {
+#pragma unroll
+            for (int x = 0; x < 5; x++) {
+                al[y + x] = kchi(bl[y + x], bl[y + (x + 1) % 5], bl[y + (x + 2) % 5]);
+                ah[y + x] = kchi(bh[y + x], bh[y + (x + 1) % 5], bh[y + (x + 2) % 5]);
+            }
+        }
+        al[0] ^= (uint32_t)KECCAK_RC[round];
+        ah[0] ^= (uint32_t)(KECCAK_RC[round] >> 32);
     }
+}
+
+GSV_DI void keccakf(uint64_t a[25]) {
+    uint32_t al[25], ah[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) {
+        al[k] = (uint32_t)a[k];
+        ah[k] = (uint32_t)(a[k] >> 32);
+    }
+    keccakf_split(al, ah);
+#pragma unroll
+    for (int k = 0; k < 25; k++) a[k] = (uint64_t)al[k] | ((uint64_t)ah[k] << 32);
 }
 
 // Keccak-256 of the 64-byte string X||Y given as big-endian 256-bit limb arrays
