@@ -50,7 +50,7 @@ PERMS_PER_MIB = 83016      # Keccak-f permutations per 1 MiB chunk root (SURVEY.
 HBM_PEAK_GBPS = 8000.0
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "latest", "pmc_summary.json")
 
 
 def pmc_traffic(kernel: str):
