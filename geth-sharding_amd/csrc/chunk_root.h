@@ -12,6 +12,11 @@
 //   kind BRANCH / EXT / LEAF  generic nodes (partial right edge, top of trie, root): assembled
 //                byte by byte from children refs, inlined when RLP < 32 bytes (trie/hasher.go:163),
 //                the root always hashed (force).
+//
+// GENERIC plans serve DeriveSha over any DerivableList (tx root core/block_validator.go:70, receipt
+// root :92): the same key-only shape, but values are arbitrary byte strings (list.GetRlp(j)), so no
+// BOTTOM/HFULL specialisation — every leaf is hashed or inlined by k_derive_leaf at the depth the
+// plan records (leaf_depth[j]) and every internal node is a generic BRANCH/EXT.
 #pragma once
 #include <stdint.h>
 
@@ -51,6 +56,8 @@ constexpr int REF_STRIDE = 48;   // bytes per ref slot: [0] = length, [8..41) = 
 
 struct TriePlanHost {
     uint32_t N = 0;
+    bool generic = false;
+    std::vector<uint16_t> leaf_depth;  // generic: nibble index where leaf j's remainder key starts
     std::vector<PNode> nodes;     // sorted by height, BOTTOM first inside height 1
     std::vector<PChild> children;
     // per height h (1..H): [bottom_begin, bottom_end) and [gen_begin, gen_end) node id ranges
@@ -65,19 +72,20 @@ struct TriePlan {
     TriePlanHost h;
     PNode* d_nodes = nullptr;
     PChild* d_children = nullptr;
+    uint16_t* d_leaf_depth = nullptr;
 };
 
-void build_trie_plan(TriePlanHost& p, uint32_t N);
+void build_trie_plan(TriePlanHost& p, uint32_t N, bool generic = false);
 
 class PlanCache {
   public:
     ~PlanCache();
     // returns a device-resident plan for length N (built and uploaded on first use)
-    TriePlan* get(uint32_t N);
+    TriePlan* get(uint32_t N, bool generic = false);
 
   private:
     std::mutex mu_;
-    std::map<uint32_t, std::unique_ptr<TriePlan>> plans_;
+    std::map<uint64_t, std::unique_ptr<TriePlan>> plans_;
 };
 
 }  // namespace gsv

@@ -20,7 +20,7 @@ namespace gsv {
 // ================================================================ key helpers (host + device)
 // nibbles of keybytesToHex(rlp(uint(i))) including the terminator 16
 __host__ __device__ inline int key_nbytes(uint32_t i) {
-    return i < 128 ? 1 : i < 256 ? 2 : i < 65536 ? 3 : 4;  // i == 0 -> [0x80] (1 byte)
+    return i < 128 ? 1 : i < 256 ? 2 : i < 65536 ? 3 : i < (1u << 24) ? 4 : 5;  // i == 0 -> [0x80] (1 byte)
 }
 __host__ __device__ inline uint8_t key_byte(uint32_t i, int b) {
     int nb = key_nbytes(i);
@@ -42,6 +42,8 @@ namespace {
 struct Builder {
     uint32_t N;
     uint32_t nB;  // keys 1..127 present (they sort first)
+    bool generic = false;
+    std::vector<uint16_t>* leaf_depth = nullptr;  // generic: depth per body index
     std::vector<PNode> nodes;
     std::vector<std::vector<PChild>> kids;
 
@@ -72,7 +74,10 @@ struct Builder {
     }
 
     Res build(uint32_t lo, uint32_t hi, int depth) {
-        if (hi - lo == 1) return Res{true, ipos(lo), (uint16_t)depth, -1, 0};
+        if (hi - lo == 1) {
+            if (generic) (*leaf_depth)[ipos(lo)] = (uint16_t)depth;
+            return Res{true, ipos(lo), (uint16_t)depth, -1, 0};
+        }
         uint32_t fi = ipos(lo), la = ipos(hi - 1);
         int cp = depth;
         while (key_nib(fi, cp) == key_nib(la, cp)) cp++;
@@ -106,7 +111,7 @@ struct Builder {
         }
         starts[nch] = hi;
         // full bottom branch: 16 single keys whose remainder after this nibble is the terminator
-        if (nch == 16 && hi - lo == 16) {
+        if (!generic && nch == 16 && hi - lo == 16) {
             bool bottom = true;
             for (uint32_t p = lo; p < hi && bottom; p++) bottom = key_len(ipos(p)) - 1 == depth + 1;
             if (bottom) {
@@ -119,7 +124,7 @@ struct Builder {
         }
         std::vector<PChild> ch;
         int h = 0;
-        bool all_hashed_full = (nch == 16);
+        bool all_hashed_full = !generic && (nch == 16);
         for (int c = 0; c < nch; c++) {
             Res r = build(starts[c], starts[c + 1], depth + 1);
             if (r.leaf) {
@@ -143,14 +148,21 @@ struct Builder {
 
 }  // namespace
 
-void build_trie_plan(TriePlanHost& p, uint32_t N) {
+void build_trie_plan(TriePlanHost& p, uint32_t N, bool generic) {
     p = TriePlanHost();
     p.N = N;
+    p.generic = generic;
     if (N == 0) return;
     Builder b;
     b.N = N;
     b.nB = N > 128 ? 127 : N - 1;
+    b.generic = generic;
+    if (generic) {
+        p.leaf_depth.assign(N, 0);
+        b.leaf_depth = &p.leaf_depth;
+    }
     Builder::Res r = b.build(0, N, 0);
+    if (generic && r.leaf) return;  // N == 1: k_derive_leaf hashes the lone leaf as the root
     int root;
     if (r.leaf) {  // N == 1: a single leaf is the root
         root = b.new_node(PK_LEAF);
@@ -224,15 +236,23 @@ PlanCache::~PlanCache() {
     for (auto& kv : plans_) {
         if (kv.second->d_nodes) (void)hipFree(kv.second->d_nodes);
         if (kv.second->d_children) (void)hipFree(kv.second->d_children);
+        if (kv.second->d_leaf_depth) (void)hipFree(kv.second->d_leaf_depth);
     }
 }
 
-TriePlan* PlanCache::get(uint32_t N) {
+TriePlan* PlanCache::get(uint32_t N, bool generic) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = plans_.find(N);
+    uint64_t key = (uint64_t)N | (generic ? (1ull << 32) : 0ull);
+    auto it = plans_.find(key);
     if (it != plans_.end()) return it->second.get();
     auto pl = std::make_unique<TriePlan>();
-    build_trie_plan(pl->h, N);
+    build_trie_plan(pl->h, N, generic);
+    if (!pl->h.leaf_depth.empty()) {
+        size_t nb = pl->h.leaf_depth.size() * sizeof(uint16_t);
+        if (hipMalloc(&pl->d_leaf_depth, nb) != hipSuccess) return nullptr;
+        if (hipMemcpy(pl->d_leaf_depth, pl->h.leaf_depth.data(), nb, hipMemcpyHostToDevice) != hipSuccess)
+            return nullptr;
+    }
     if (!pl->h.nodes.empty()) {
         if (hipMalloc(&pl->d_nodes, pl->h.nodes.size() * sizeof(PNode)) != hipSuccess) return nullptr;
         if (hipMemcpy(pl->d_nodes, pl->h.nodes.data(), pl->h.nodes.size() * sizeof(PNode),
@@ -246,7 +266,7 @@ TriePlan* PlanCache::get(uint32_t N) {
         }
     }
     TriePlan* r = pl.get();
-    plans_[N] = std::move(pl);
+    plans_[key] = std::move(pl);
     return r;
 }
 
@@ -259,6 +279,10 @@ struct BodyBatch {
     uint8_t* roots;            // 32 B per body
     uint64_t msg_stride, ref_stride;
     uint32_t nbodies;
+    // generic DeriveSha: leaf j of list b has its reference at leafrefs + (leaf_base[b] + j) * REF_STRIDE
+    const uint8_t* leafrefs;
+    const uint64_t* leaf_base;
+    int generic;
 };
 
 // Keccak-256 of len bytes at p (8-byte aligned; bytes past len may be garbage)
@@ -461,7 +485,11 @@ GSV_DI void write_leaf(Writer& w, uint32_t i, int d, uint8_t b) {
 
 GSV_DI void write_child_ref(Writer& w, const BodyBatch& bb, uint32_t body, const PChild& c,
                             const PNode* nodes) {
-    if (c.type == PC_LEAF) {
+    if (c.type == PC_LEAF && bb.generic) {
+        const uint8_t* s = bb.leafrefs + (bb.leaf_base[body] + c.idx) * REF_STRIDE;
+        uint32_t len = s[0];
+        for (uint32_t k = 0; k < len; k++) w.put(s[8 + k]);
+    } else if (c.type == PC_LEAF) {
         uint8_t b = bb.bodies[bb.body_off[body] + c.idx];
         write_leaf(w, c.idx, c.depth, b);
     } else {
@@ -569,6 +597,9 @@ hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies,
     bb.refs = d_scratch + bb.msg_stride * nbodies;
     bb.roots = d_roots;
     bb.nbodies = nbodies;
+    bb.leafrefs = nullptr;
+    bb.leaf_base = nullptr;
+    bb.generic = 0;
     for (int h = 1; h <= p.height; h++) {
         int b0 = p.lvl_bottom_begin[h - 1], b1 = p.lvl_bottom_end[h - 1];
         if (b1 > b0) {
@@ -590,6 +621,162 @@ hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies,
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// ================================================================ generic DeriveSha (any DerivableList)
+// RLP length prefix for a string (base 0x80) or list (base 0xc0) of `len` bytes (rlp/encode.go:71-89)
+GSV_DI void put_prefix(Writer& w, uint8_t base, uint32_t len) {
+    if (len < 56) {
+        w.put((uint8_t)(base + len));
+        return;
+    }
+    int nb = len < 256 ? 1 : len < 65536 ? 2 : len < (1u << 24) ? 3 : 4;
+    w.put((uint8_t)(base + 55 + nb));
+    for (int k = nb - 1; k >= 0; k--) w.put((uint8_t)(len >> (8 * k)));
+}
+GSV_DI uint32_t prefix_len(uint32_t len) {
+    return len < 56 ? 1u : len < 256 ? 2u : len < 65536 ? 3u : len < (1u << 24) ? 4u : 5u;
+}
+
+// One lane per leaf: leaf j of list b = shortNode{hexToCompact(key(j)[depth:]), valueNode(GetRlp(j))}
+// encoded [compact, string(value)] (trie/hasher.go:113-145 via node.go EncodeRLP); inlined into its
+// parent when the RLP is < 32 bytes, else hashed; a list of one item is that leaf, hashed as root.
+__global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__ vals,
+                                                     const uint64_t* __restrict__ voff,
+                                                     const uint64_t* __restrict__ lmsg_off, uint8_t* lmsg,
+                                                     const uint64_t* __restrict__ leaf_base,
+                                                     const uint16_t* __restrict__ leaf_depth, uint32_t N,
+                                                     uint32_t nlists, uint8_t* leafrefs, uint8_t* roots) {
+    uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (uint64_t)N * nlists) return;
+    uint32_t b = (uint32_t)(t / N), j = (uint32_t)(t % N);
+    uint64_t item = leaf_base[b] + j;
+    const uint8_t* v = vals + voff[item];
+    uint32_t L = (uint32_t)(voff[item + 1] - voff[item]);
+    int depth = leaf_depth[j];
+    uint8_t ck[8];
+    int cl = compact_key(ck, j, depth, key_len(j));
+    uint32_t kenc = (cl == 1 && ck[0] < 0x80) ? 1u : 1u + cl;
+    bool vbyte = (L == 1 && v[0] < 0x80);
+    uint32_t venc = vbyte ? 1u : prefix_len(L) + L;
+    uint8_t* m = lmsg + lmsg_off[item];
+    Writer w{m, 0, false};
+    put_prefix(w, 0xc0, kenc + venc);
+    w.str(ck, cl);
+    if (vbyte) {
+        w.put(v[0]);
+    } else {
+        put_prefix(w, 0x80, L);
+        for (uint32_t k = 0; k < L; k++) w.put(v[k]);
+    }
+    uint32_t len = w.n;
+    uint8_t* s = leafrefs + item * REF_STRIDE;
+    if (N == 1 || len >= 32) {
+        uint32_t h[8];
+        keccak_buf(h, m, len);
+        if (N == 1) {
+            uint8_t* o = roots + (size_t)b * 32;
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+#pragma unroll
+                for (int y = 0; y < 4; y++) o[4 * q + y] = (uint8_t)(h[q] >> (8 * y));
+        } else {
+            s[0] = 33;
+            put_hashref(s + 8, h);
+        }
+    } else {
+        s[0] = (uint8_t)len;
+        for (uint32_t k = 0; k < len; k++) s[8 + k] = m[k];
+    }
+}
+
+size_t derive_sha_scratch_bytes(const TriePlan* plan, uint32_t nlists) {
+    return plan->h.nodes.empty() ? 512 : chunk_root_scratch_bytes(plan, nlists);
+}
+
+hipError_t launch_derive_sha_plan(const TriePlan* plan, uint32_t nlists, const uint8_t* d_vals,
+                                  const uint64_t* d_voff, const uint64_t* d_leaf_base, const uint64_t* d_lmsg_off,
+                                  uint8_t* d_lmsg, uint8_t* d_leafrefs, uint8_t* d_scratch, uint8_t* d_roots,
+                                  hipStream_t st, void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
+                                  void* tctx) {
+    const TriePlanHost& p = plan->h;
+    if (nlists == 0 || p.N == 0 || !p.generic) return hipSuccess;
+    uint64_t total = (uint64_t)p.N * nlists;
+    if (timer_begin) timer_begin(tctx, GSV_K_DERIVE_LEAF);
+    hipLaunchKernelGGL(k_derive_leaf, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d_vals, d_voff,
+                       d_lmsg_off, d_lmsg, d_leaf_base, plan->d_leaf_depth, p.N, nlists, d_leafrefs, d_roots);
+    if (timer_end) timer_end(tctx, GSV_K_DERIVE_LEAF);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || p.nodes.empty()) return e;
+    BodyBatch bb;
+    bb.bodies = nullptr;
+    bb.body_off = nullptr;
+    bb.msg_stride = (size_t)p.n_msg * MSG_STRIDE;
+    bb.ref_stride = (size_t)p.n_slots * REF_STRIDE;
+    bb.msg = d_scratch;
+    bb.refs = d_scratch + bb.msg_stride * nlists;
+    bb.roots = d_roots;
+    bb.nbodies = nlists;
+    bb.leafrefs = d_leafrefs;
+    bb.leaf_base = d_leaf_base;
+    bb.generic = 1;
+    for (int h = 1; h <= p.height; h++) {
+        int g0 = p.lvl_gen_begin[h - 1], g1 = p.lvl_gen_end[h - 1];
+        if (g1 <= g0) continue;
+        uint64_t tot = (uint64_t)(g1 - g0) * nlists;
+        if (timer_begin) timer_begin(tctx, GSV_K_CHUNK_LEVEL);
+        hipLaunchKernelGGL(k_chunk_level, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, plan->d_nodes,
+                           plan->d_children, g0, g1 - g0, bb);
+        if (timer_end) timer_end(tctx, GSV_K_CHUNK_LEVEL);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// ================================================================ Proof of Custody body expansion
+// sharding/collation.go:124-136: salted[k*(s+1) .. +s) = salt, salted[k*(s+1)+s] = body[k]; an empty
+// body gives salted = salt.  One thread per 4 output bytes, grid.y = body; in_off holds (start, end)
+// pairs per body, out_off the 16-byte aligned output starts.
+__global__ __launch_bounds__(256) void k_poc_expand(const uint8_t* __restrict__ bodies,
+                                                    const uint64_t* __restrict__ in_off,
+                                                    const uint64_t* __restrict__ out_off,
+                                                    const uint8_t* __restrict__ salt, uint32_t slen,
+                                                    uint8_t* out) {
+    uint32_t b = blockIdx.y;
+    uint64_t n_in = in_off[2 * b + 1] - in_off[2 * b];
+    uint64_t n_out = n_in ? n_in * (slen + 1) : slen;
+    uint64_t k0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (k0 >= n_out) return;
+    const uint8_t* src = bodies + in_off[2 * b];
+    uint8_t* dst = out + out_off[b];
+    uint64_t q = k0 / (slen + 1);
+    uint32_t r = (uint32_t)(k0 - q * (slen + 1));
+    uint8_t o[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        o[u] = k0 + u >= n_out ? 0 : (!n_in || r < slen) ? salt[r] : src[q];
+        if (++r > slen) {
+            r = 0;
+            q++;
+        }
+    }
+    if (k0 + 4 <= n_out) {
+        *(uint32_t*)(dst + k0) = (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) |
+                                 ((uint32_t)o[3] << 24);
+    } else {
+        for (uint64_t u = 0; k0 + u < n_out; u++) dst[k0 + u] = o[u];
+    }
+}
+
+hipError_t launch_poc_expand(const uint8_t* d_bodies, const uint64_t* d_in_off, const uint64_t* d_out_off,
+                             uint32_t nbodies, uint64_t max_out, const uint8_t* d_salt, uint32_t slen, uint8_t* d_out,
+                             hipStream_t st) {
+    if (!nbodies || !max_out) return hipSuccess;
+    uint64_t blocks = (max_out + 1023) / 1024;
+    hipLaunchKernelGGL(k_poc_expand, dim3((unsigned)blocks, nbodies), dim3(256), 0, st, d_bodies, d_in_off,
+                       d_out_off, d_salt, slen, d_out);
+    return hipGetLastError();
 }
 
 }  // namespace gsv

@@ -40,6 +40,8 @@ struct gsv_ctx {
     std::mutex wmu;                   // serializes users of `work`
     uint8_t* nwork = nullptr;         // notary workspace (blob tables, chain-id buffers)
     size_t nwork_cap = 0;
+    uint8_t* pwork = nullptr;         // Proof-of-Custody salted bodies (outlive `work` regrowth)
+    size_t pwork_cap = 0;
 };
 
 namespace {
@@ -229,6 +231,7 @@ void gsv_ctx_destroy(gsv_ctx* c) {
     if (c->arena) hipFree(c->arena);
     if (c->work) hipFree(c->work);
     if (c->nwork) hipFree(c->nwork);
+    if (c->pwork) hipFree(c->pwork);
     if (c->gtab) hipFree(c->gtab);
     hipStreamDestroy(c->stream);
     delete c;
@@ -408,11 +411,12 @@ static const uint64_t MAX_BODY = 1ull << 20;  // collationSizelimit (sharding/co
 
 // Body i = d_bodies[start[i] .. end[i]); roots to d_roots (device) via workspace `work`.
 static int chunk_root_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* start,
-                               const uint64_t* end, size_t n, uint8_t* d_roots, hipStream_t st) {
+                               const uint64_t* end, size_t n, uint8_t* d_roots, hipStream_t st,
+                               uint64_t max_len = MAX_BODY) {
     // group bodies by length (the trie shape depends only on N)
     std::map<uint64_t, std::vector<uint32_t>> groups;
     for (size_t i = 0; i < n; i++) {
-        if (end[i] < start[i] || end[i] - start[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+        if (end[i] < start[i] || end[i] - start[i] > max_len) return GSV_E_TOO_LARGE;
         groups[end[i] - start[i]].push_back((uint32_t)i);
     }
     size_t need = 0;
@@ -834,6 +838,251 @@ int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t
     HIPCHK(hipStreamSynchronize(c->stream));
     for (size_t i = 0; i < n_shards; i++)
         if (ntx_out[i] > max_txs) return GSV_E_TOO_LARGE;
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ DeriveSha over any DerivableList
+static const uint64_t MAX_LIST = 1ull << 24;
+
+// item k = d_vals[voff[k] .. voff[k+1]); list i = items [list_off[i], list_off[i+1])
+static int derive_sha_dev_impl(gsv_ctx* c, const uint8_t* d_vals, const uint64_t* voff, const uint64_t* list_off,
+                               size_t n, uint8_t* d_roots, hipStream_t st) {
+    std::map<uint64_t, std::vector<uint32_t>> groups;
+    for (size_t i = 0; i < n; i++) {
+        if (list_off[i + 1] < list_off[i]) return GSV_E_INVALID_ARG;
+        uint64_t N = list_off[i + 1] - list_off[i];
+        if (N > MAX_LIST) return GSV_E_TOO_LARGE;
+        groups[N].push_back((uint32_t)i);
+    }
+    uint64_t total = list_off[n] - list_off[0];
+    for (uint64_t k = list_off[0]; k < list_off[n]; k++)
+        if (voff[k + 1] < voff[k] || voff[k + 1] - voff[k] >= (1ull << 32)) return GSV_E_INVALID_ARG;
+    // per item: message buffer offset (8-aligned, value + 24 bytes of RLP headers) and ref slot
+    std::vector<uint64_t> lmsg(total + 1);
+    uint64_t pos = 0;
+    for (uint64_t k = 0; k < total; k++) {
+        lmsg[k] = pos;
+        pos += (voff[list_off[0] + k + 1] - voff[list_off[0] + k] + 24 + 7) & ~7ull;
+    }
+    size_t need = al((total + 1) * 8) * 2 + al(pos + 256) + al(total * 48);
+    for (auto& g : groups) {
+        if (g.first == 0) continue;
+        gsv::TriePlan* pl = c->plans.get((uint32_t)g.first, true);
+        if (!pl) return GSV_E_NOMEM;
+        need += al(g.second.size() * 8) + al(g.second.size() * 32) +
+                al(gsv::derive_sha_scratch_bytes(pl, (uint32_t)g.second.size()));
+    }
+    int rc = work_reserve(c, need + 4096);
+    if (rc) return rc;
+    Carve cv(c->work);
+    c->cur_stream = st;
+    // voff rebased to d_vals is what the caller gave; items indexed from list_off[0]
+    uint64_t* d_voff = cv.take<uint64_t>((total + 1) * 8);
+    uint64_t* d_lmsg_off = cv.take<uint64_t>((total + 1) * 8);
+    uint8_t* d_lmsg = cv.take<uint8_t>(pos + 256);
+    uint8_t* d_leafrefs = cv.take<uint8_t>(total * 48);
+    HIPCHK(hipMemcpyAsync(d_voff, voff + list_off[0], (total + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_lmsg_off, lmsg.data(), (total + 1) * 8, hipMemcpyHostToDevice, st));
+    std::vector<std::vector<uint64_t>> host_base;
+    host_base.reserve(groups.size());
+    for (auto& g : groups) {
+        const auto& idx = g.second;
+        if (g.first == 0) {  // empty list -> emptyRoot (trie/trie.go:472-474)
+            for (uint32_t i : idx)
+                HIPCHK(hipMemcpyAsync(d_roots + (size_t)i * 32, EMPTY_ROOT, 32, hipMemcpyHostToDevice, st));
+            continue;
+        }
+        gsv::TriePlan* pl = c->plans.get((uint32_t)g.first, true);
+        uint64_t* d_base = cv.take<uint64_t>(idx.size() * 8);
+        uint8_t* d_gr = cv.take<uint8_t>(idx.size() * 32);
+        uint8_t* d_scr = cv.take<uint8_t>(gsv::derive_sha_scratch_bytes(pl, (uint32_t)idx.size()));
+        host_base.emplace_back(idx.size());
+        auto& hb = host_base.back();
+        for (size_t k = 0; k < idx.size(); k++) hb[k] = list_off[idx[k]] - list_off[0];
+        HIPCHK(hipMemcpyAsync(d_base, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(gsv::launch_derive_sha_plan(pl, (uint32_t)idx.size(), d_vals, d_voff, d_base, d_lmsg_off, d_lmsg,
+                                           d_leafrefs, d_scr, d_gr, st, hook_begin, hook_end, c));
+        size_t k = 0;
+        while (k < idx.size()) {
+            size_t e2 = k + 1;
+            while (e2 < idx.size() && idx[e2] == idx[e2 - 1] + 1) e2++;
+            HIPCHK(hipMemcpyAsync(d_roots + (size_t)idx[k] * 32, d_gr + k * 32, (e2 - k) * 32,
+                                  hipMemcpyDeviceToDevice, st));
+            k = e2;
+        }
+    }
+    HIPCHK(hipStreamSynchronize(st));  // host staging must outlive the async copies
+    return GSV_SUCCESS;
+}
+
+int gsv_derive_sha_batch_dev(gsv_ctx* c, const uint8_t* d_vals, const uint64_t* voff, const uint64_t* list_off,
+                             size_t n, uint8_t* d_root32_out, void* stream) {
+    if (!c || (n && (!voff || !list_off || !d_root32_out))) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    if (list_off[n] > list_off[0] && !d_vals) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->wmu);
+    HIPCHK(hipSetDevice(c->device));
+    return derive_sha_dev_impl(c, d_vals, voff, list_off, n, d_root32_out, stream ? (hipStream_t)stream : c->stream);
+}
+
+int gsv_derive_sha_batch(gsv_ctx* c, const uint8_t* vals, const uint64_t* voff, const uint64_t* list_off, size_t n,
+                         uint8_t* root32_out) {
+    if (!c || (n && (!voff || !list_off || !root32_out))) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    if (list_off[n] < list_off[0]) return GSV_E_INVALID_ARG;
+    uint64_t v0 = voff[list_off[0]], v1 = voff[list_off[n]];
+    if (v1 < v0 || (v1 > v0 && !vals)) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    // stage the values (rebased so item list_off[0] starts at 0)
+    std::vector<uint64_t> rv(list_off[n] + 1, 0);
+    for (uint64_t k = list_off[0]; k <= list_off[n]; k++) rv[k] = voff[k] - v0;
+    int rc = arena_reserve(c, al(v1 - v0 + 16) + al(n * 32));
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_v = cv.take<uint8_t>(v1 - v0 + 16);
+    uint8_t* d_r = cv.take<uint8_t>(n * 32);
+    if (v1 > v0) HIPCHK(hipMemcpyAsync(d_v, vals + v0, v1 - v0, hipMemcpyHostToDevice, c->stream));
+    {
+        std::lock_guard<std::mutex> g2(c->wmu);
+        rc = derive_sha_dev_impl(c, d_v, rv.data(), list_off, n, d_r, c->stream);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(root32_out, d_r, n * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ Proof of Custody
+static const uint64_t MAX_POC = 1ull << 26;
+
+static int poc_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* start, const uint64_t* end, size_t n,
+                        const uint8_t* salt, size_t slen, uint8_t* d_poc, hipStream_t st) {
+    std::vector<uint64_t> io(2 * n), oo(n), os(n), oe(n);
+    uint64_t pos = 0, mx = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (end[i] < start[i]) return GSV_E_INVALID_ARG;
+        uint64_t L = end[i] - start[i];
+        if (L > MAX_POC) return GSV_E_TOO_LARGE;
+        uint64_t N = L ? L * (slen + 1) : slen;
+        if (N > MAX_POC) return GSV_E_TOO_LARGE;
+        io[2 * i] = start[i];
+        io[2 * i + 1] = end[i];
+        oo[i] = os[i] = pos;
+        oe[i] = pos + N;
+        mx = N > mx ? N : mx;
+        pos = (oe[i] + 15) & ~15ull;
+    }
+    size_t need = al(pos + 16) + al(2 * n * 8) + al(n * 8) + al(slen + 1);
+    if (need > c->pwork_cap) {
+        size_t cap = c->pwork_cap ? c->pwork_cap : (size_t)64 << 20;
+        while (cap < need) cap *= 2;
+        if (c->pwork) {
+            hipDeviceSynchronize();
+            hipFree(c->pwork);
+            c->pwork = nullptr;
+            c->pwork_cap = 0;
+        }
+        if (hipMalloc(&c->pwork, cap) != hipSuccess) return GSV_E_NOMEM;
+        c->pwork_cap = cap;
+    }
+    Carve cv(c->pwork);
+    uint8_t* d_out = cv.take<uint8_t>(pos + 16);
+    uint64_t* d_io = cv.take<uint64_t>(2 * n * 8);
+    uint64_t* d_oo = cv.take<uint64_t>(n * 8);
+    uint8_t* d_salt = cv.take<uint8_t>(slen + 1);
+    HIPCHK(hipMemcpyAsync(d_io, io.data(), 2 * n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_oo, oo.data(), n * 8, hipMemcpyHostToDevice, st));
+    if (slen) HIPCHK(hipMemcpyAsync(d_salt, salt, slen, hipMemcpyHostToDevice, st));
+    HIPCHK(gsv::launch_poc_expand(d_bodies, d_io, d_oo, (uint32_t)n, mx, d_salt, (uint32_t)slen, d_out, st));
+    int rc = chunk_root_dev_impl(c, d_out, os.data(), oe.data(), n, d_poc, st, MAX_POC);
+    return rc;  // chunk_root_dev_impl synchronizes the stream before returning
+}
+
+int gsv_collation_poc_batch_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n,
+                                const uint8_t* salt, size_t salt_len, uint8_t* d_poc32_out, void* stream) {
+    if (!c || (n && (!h_off || !d_poc32_out)) || (salt_len && !salt)) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->wmu);
+    HIPCHK(hipSetDevice(c->device));
+    return poc_dev_impl(c, d_bodies, h_off, h_off + 1, n, salt, salt_len, d_poc32_out,
+                        stream ? (hipStream_t)stream : c->stream);
+}
+
+int gsv_collation_poc_batch(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n, const uint8_t* salt,
+                            size_t salt_len, uint8_t* poc32_out) {
+    if (!c || (n && (!off || !poc32_out)) || (salt_len && !salt)) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    for (size_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_POC) return GSV_E_TOO_LARGE;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint64_t> st(n), en(n);
+    uint64_t pos = 0;
+    for (size_t i = 0; i < n; i++) {
+        st[i] = pos;
+        en[i] = pos + (off[i + 1] - off[i]);
+        pos = (en[i] + 15) & ~15ull;
+    }
+    int rc = arena_reserve(c, al(pos + 16) + al(n * 32));
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_b = cv.take<uint8_t>(pos + 16);
+    uint8_t* d_r = cv.take<uint8_t>(n * 32);
+    for (size_t i = 0; i < n; i++)
+        if (en[i] > st[i])
+            HIPCHK(hipMemcpyAsync(d_b + st[i], bodies + off[i], en[i] - st[i], hipMemcpyHostToDevice, c->stream));
+    {
+        std::lock_guard<std::mutex> g2(c->wmu);
+        rc = poc_dev_impl(c, d_b, st.data(), en.data(), n, salt, salt_len, d_r, c->stream);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(poc32_out, d_r, n * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ collation header + proposer signature
+int gsv_collation_header_verify_batch(gsv_ctx* c, const uint8_t* shard_id32, const uint8_t* chunk_root32,
+                                      const uint8_t* period32, const uint8_t* proposer20, const uint8_t* sig65,
+                                      const uint8_t* nil_flags, size_t n, uint8_t* hash32_out,
+                                      uint8_t* signer20_out, uint8_t* status) {
+    if (!c || (n && (!shard_id32 || !chunk_root32 || !period32 || !proposer20 || !sig65 || !status)))
+        return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    if (n > (1u << 30)) return GSV_E_TOO_LARGE;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    int rc = arena_reserve(c, al(n * 32) * 4 + al(n * 20) * 2 + al(n * 65) + al(n) * 2 +
+                                  al(gsv::header_scratch_bytes((uint32_t)n)));
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_sid = cv.take<uint8_t>(n * 32);
+    uint8_t* d_root = cv.take<uint8_t>(n * 32);
+    uint8_t* d_per = cv.take<uint8_t>(n * 32);
+    uint8_t* d_prop = cv.take<uint8_t>(n * 20);
+    uint8_t* d_sig = cv.take<uint8_t>(n * 65);
+    uint8_t* d_nil = nil_flags ? cv.take<uint8_t>(n) : nullptr;
+    uint8_t* d_hash = hash32_out ? cv.take<uint8_t>(n * 32) : nullptr;
+    uint8_t* d_signer = signer20_out ? cv.take<uint8_t>(n * 20) : nullptr;
+    uint8_t* d_st = cv.take<uint8_t>(n);
+    uint8_t* d_scr = cv.take<uint8_t>(gsv::header_scratch_bytes((uint32_t)n));
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemcpyAsync(d_sid, shard_id32, n * 32, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_root, chunk_root32, n * 32, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_per, period32, n * 32, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_prop, proposer20, n * 20, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_sig, sig65, n * 65, hipMemcpyHostToDevice, st));
+    if (d_nil) HIPCHK(hipMemcpyAsync(d_nil, nil_flags, n, hipMemcpyHostToDevice, st));
+    {
+        KTimer t(c, GSV_K_HEADER, st);
+        HIPCHK(gsv::launch_header_verify(d_sid, d_root, d_per, d_prop, d_sig, d_nil, (uint32_t)n, c->gtab, d_scr,
+                                         d_hash, d_signer, d_st, st));
+    }
+    if (hash32_out) HIPCHK(hipMemcpyAsync(hash32_out, d_hash, n * 32, hipMemcpyDeviceToHost, st));
+    if (signer20_out) HIPCHK(hipMemcpyAsync(signer20_out, d_signer, n * 20, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     return GSV_SUCCESS;
 }
 

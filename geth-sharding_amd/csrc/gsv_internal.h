@@ -29,6 +29,24 @@ hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies,
                                   void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
                                   void* tctx);
 
+// generic DeriveSha (any DerivableList) and the Proof-of-Custody salted body
+size_t derive_sha_scratch_bytes(const TriePlan* plan, uint32_t nlists);
+hipError_t launch_derive_sha_plan(const TriePlan* plan, uint32_t nlists, const uint8_t* d_vals,
+                                  const uint64_t* d_voff, const uint64_t* d_leaf_base, const uint64_t* d_lmsg_off,
+                                  uint8_t* d_lmsg, uint8_t* d_leafrefs, uint8_t* d_scratch, uint8_t* d_roots,
+                                  hipStream_t st, void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
+                                  void* tctx);
+hipError_t launch_poc_expand(const uint8_t* d_bodies, const uint64_t* d_in_off, const uint64_t* d_out_off,
+                             uint32_t nbodies, uint64_t max_out, const uint8_t* d_salt, uint32_t slen, uint8_t* d_out,
+                             hipStream_t st);
+
+// collation.hip: header hashes + proposer signature (ecrecover of the unsigned header hash)
+size_t header_scratch_bytes(uint32_t n);
+hipError_t launch_header_verify(const uint8_t* d_sid32, const uint8_t* d_root32, const uint8_t* d_per32,
+                                const uint8_t* d_prop20, const uint8_t* d_sig65, const uint8_t* d_nil, uint32_t n,
+                                const uint4* gtab, uint8_t* d_scratch, uint8_t* d_hash32, uint8_t* d_signer20,
+                                uint8_t* d_status, hipStream_t st);
+
 // bn256.hip: pair_src[p] = byte offset of pair p in d_in; pairs of check c are
 // [check_first[c], check_first[c+1]); workspaces: pstat[npairs], pts[48][npairs], fv[96][npairs] words
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,

@@ -305,3 +305,77 @@ Context.pairing_check_batch = _pairing_check_batch
 Context.pairing_check_batch_dev = _pairing_check_batch_dev
 Context.chunk_root_batch = _chunk_root_batch
 Context.chunk_root_batch_dev = _chunk_root_batch_dev
+
+
+def _derive_sha_batch(self, lists) -> np.ndarray:
+    """types.DeriveSha for each list of item RLPs (core/types/derive_sha.go:32-41): list i is a
+    sequence of byte strings, item j being list.GetRlp(j) (rlp(tx) for a block's transactions)."""
+    n = len(lists)
+    out = np.zeros((n, 32), np.uint8)
+    if n == 0:
+        return out
+    items = [bytes(x) for lst in lists for x in lst]
+    flat, voff = _pack(items)
+    list_off = np.zeros(n + 1, np.uint64)
+    list_off[1:] = np.cumsum([len(lst) for lst in lists])
+    check(_lib.load().gsv_derive_sha_batch(self._h, _ptr(flat), _ptr(voff), _ptr(list_off), n, _ptr(out)))
+    return out
+
+
+def _derive_sha_batch_dev(self, vals_t, voff, list_off, roots_t, stream=None):
+    """vals_t: torch uint8 CUDA tensor of all item bytes; voff (items+1) / list_off (lists+1): numpy uint64."""
+    voff = np.ascontiguousarray(voff, np.uint64)
+    list_off = np.ascontiguousarray(list_off, np.uint64)
+    n = list_off.shape[0] - 1
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_derive_sha_batch_dev(self._h, _tptr(vals_t), _ptr(voff), _ptr(list_off), n,
+                                               _tptr(roots_t), sp))
+
+
+def _collation_poc_batch(self, bodies, salt: bytes) -> np.ndarray:
+    """Collation.CalculatePOC(salt) for each body (sharding/collation.go:124-136)."""
+    n = len(bodies)
+    out = np.zeros((n, 32), np.uint8)
+    if n == 0:
+        return out
+    flat, off = _pack(bodies)
+    sb = np.frombuffer(bytes(salt) + b"\0", np.uint8)
+    check(_lib.load().gsv_collation_poc_batch(self._h, _ptr(flat), _ptr(off), n, _ptr(sb), len(salt), _ptr(out)))
+    return out
+
+
+def _collation_poc_batch_dev(self, bodies_t, h_off, salt: bytes, out_t, stream=None):
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    n = h_off.shape[0] - 1
+    sb = np.frombuffer(bytes(salt) + b"\0", np.uint8)
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_collation_poc_batch_dev(self._h, _tptr(bodies_t), _ptr(h_off), n, _ptr(sb), len(salt),
+                                                  _tptr(out_t), sp))
+
+
+def _collation_header_verify_batch(self, shard_id32, chunk_root32, period32, proposer20, sig65, nil_flags=None):
+    """Collation header hashes + proposer-signature check (gsv.h gsv_collation_header_verify_batch):
+    returns (hash32 (n,32), signer20 (n,20), status (n,))."""
+    sid = _np_u8(shard_id32).reshape(-1, 32)
+    n = sid.shape[0]
+    root = _np_u8(chunk_root32).reshape(n, 32)
+    per = _np_u8(period32).reshape(n, 32)
+    prop = _np_u8(proposer20).reshape(n, 20)
+    sig = _np_u8(sig65).reshape(n, 65)
+    nf = None if nil_flags is None else _np_u8(nil_flags).reshape(n)
+    h = np.zeros((n, 32), np.uint8)
+    signer = np.zeros((n, 20), np.uint8)
+    st = np.zeros(n, np.uint8)
+    if n == 0:
+        return h, signer, st
+    check(_lib.load().gsv_collation_header_verify_batch(self._h, _ptr(sid), _ptr(root), _ptr(per), _ptr(prop),
+                                                        _ptr(sig), _ptr(nf) if nf is not None else None, n,
+                                                        _ptr(h), _ptr(signer), _ptr(st)))
+    return h, signer, st
+
+
+Context.derive_sha_batch = _derive_sha_batch
+Context.derive_sha_batch_dev = _derive_sha_batch_dev
+Context.collation_poc_batch = _collation_poc_batch
+Context.collation_poc_batch_dev = _collation_poc_batch_dev
+Context.collation_header_verify_batch = _collation_header_verify_batch

@@ -24,6 +24,7 @@ ST_INVALID_CHAIN_ID = 6
 ST_INVALID_PUBKEY = 7
 ST_BAD_RLP = 8
 ST_BN_BAD_INPUT = 9
+ST_PROPOSER_MISMATCH = 10
 
 SIGNER_EIP155 = 0
 SIGNER_HOMESTEAD = 1
@@ -42,6 +43,8 @@ K_SENDER_PREP = 5
 K_BN_PREPARE = 6
 K_BN_FINAL = 7
 K_NOTARY = 8
+K_DERIVE_LEAF = 9
+K_HEADER = 10
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -79,6 +82,11 @@ SIGNATURES = [
                                                       ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("gsv_notary_synth_dev", ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32, _sz, ctypes.c_uint32, _vp, _vp,
                                             _vp, _vp]),
+    ("gsv_derive_sha_batch", ctypes.c_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
+    ("gsv_derive_sha_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+    ("gsv_collation_poc_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp]),
+    ("gsv_collation_poc_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp]),
+    ("gsv_collation_header_verify_batch", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
 ]
 
 _lib = None

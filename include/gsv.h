@@ -21,6 +21,12 @@
  *                                 as driven by the bn256Pairing precompile (core/vm/contracts.go:333-360)
  *   gsv_notary_validate_shards <- the notary's per-collation validation (sharding/notary/notary.go:413-496
  *                                 + sharding/collation.go:193-206 DeserializeBlobToTx + Sender)
+ *   gsv_derive_sha_batch       <- types.DeriveSha(list) (core/types/derive_sha.go:32-41) for any
+ *                                 DerivableList: tx root (core/block_validator.go:70), receipt root (:92)
+ *   gsv_collation_poc_batch    <- Collation.CalculatePOC(salt) (sharding/collation.go:124-136)
+ *   gsv_collation_header_verify_batch <- CollationHeader.Hash (sharding/collation.go:66-71) and the
+ *                                 proposer signature made by SMCClient.Sign (sharding/mainchain/
+ *                                 smc_client.go:245-248, signed at sharding/proposer/proposer.go:83)
  *
  * Conventions
  *   - Return value: GSV_SUCCESS (0) or a negative GSV_E_* API/HIP error. A bad ITEM never fails
@@ -63,6 +69,7 @@ extern "C" {
 #define GSV_ST_INVALID_PUBKEY 7    /* "invalid public key"             transaction_signing.go:240 */
 #define GSV_ST_BAD_RLP 8           /* rlp decode error of the tx */
 #define GSV_ST_BN_BAD_INPUT 9      /* bn256 unmarshal / curve / subgroup failure */
+#define GSV_ST_PROPOSER_MISMATCH 10 /* recovered signer != header ProposerAddress */
 
 /* signer kinds for gsv_tx_sender_batch (core/types/transaction_signing.go) */
 #define GSV_SIGNER_EIP155 0
@@ -98,6 +105,8 @@ int gsv_ctx_set_timing(gsv_ctx *ctx, int enable);
 #define GSV_K_BN_PREPARE 6 /* pair decode + G1 curve + G2 subgroup checks */
 #define GSV_K_BN_FINAL 7   /* per-check product + final exponentiation */
 #define GSV_K_NOTARY 8     /* blob index + per-tx decode/sighash/recover of the notary path */
+#define GSV_K_DERIVE_LEAF 9 /* generic DeriveSha leaf encode + hash */
+#define GSV_K_HEADER 10    /* collation header hashing + signer comparison */
 #define GSV_K_COUNT 12
 /* total milliseconds and launch count accumulated for kernel `kid` since the last reset */
 int gsv_ctx_kernel_time(gsv_ctx *ctx, int kid, double *total_ms, long *launches);
@@ -196,6 +205,42 @@ int gsv_notary_validate_shards_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const 
  * (high-s / wrong chain id / r not an x-coordinate).  Optional expected status and sender per tx. */
 int gsv_notary_synth_dev(gsv_ctx *ctx, uint64_t seed, uint32_t shard0, size_t n_shards, uint32_t txs_per_shard,
                          uint8_t *d_bodies, uint8_t *d_exp_status, uint8_t *d_exp_sender, void *stream);
+
+/* ---- DeriveSha over any DerivableList (tx root, receipt root) ----
+ * List i holds items [list_off[i], list_off[i+1]) of the global item array; item k =
+ * vals[voff[k] .. voff[k+1]) is list.GetRlp(j) — the RLP the reference inserts under key rlp(j)
+ * (core/types/derive_sha.go:36-38; rlp(tx) for Transactions, rlp(receipt) for Receipts).
+ * root32_out[i] = DeriveSha(list i); an empty list gives emptyRoot.  Lists of up to 2^24 items. */
+int gsv_derive_sha_batch(gsv_ctx *ctx, const uint8_t *vals, const uint64_t *voff, const uint64_t *list_off,
+                         size_t n_lists, uint8_t *root32_out);
+/* Device-resident form: d_vals in HBM; voff / list_off on the host (offsets into d_vals / item
+ * indices); d_root32_out in HBM; enqueues on `stream` (NULL = the context stream). */
+int gsv_derive_sha_batch_dev(gsv_ctx *ctx, const uint8_t *d_vals, const uint64_t *voff, const uint64_t *list_off,
+                             size_t n_lists, uint8_t *d_root32_out, void *stream);
+
+/* ---- Proof of Custody (sharding/collation.go:124-136) ----
+ * poc32_out[i] = DeriveSha(Chunks(salt||b0||salt||b1||...)) over body i = bodies[off[i] .. off[i+1])
+ * (salt alone for an empty body).  The salted body may hold up to 2^26 bytes (GSV_E_TOO_LARGE). */
+int gsv_collation_poc_batch(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off, size_t n,
+                            const uint8_t *salt, size_t salt_len, uint8_t *poc32_out);
+int gsv_collation_poc_batch_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off, size_t n,
+                                const uint8_t *salt, size_t salt_len, uint8_t *d_poc32_out, void *stream);
+
+/* ---- collation header hash + proposer signature ----
+ * Header i = collationHeaderData{ShardID, ChunkRoot, Period, ProposerAddress, ProposerSignature}
+ * (sharding/collation.go:35-43): shard_id32 / period32 are 32-byte big-endian integers,
+ * chunk_root32, proposer20, sig65 = [R || S || V] as crypto.Sign returns it (V in {0,1}).
+ * nil_flags (optional, NULL = all set): bit 0 = ChunkRoot nil, bit 1 = ProposerAddress nil,
+ * bit 2 = ProposerSignature nil/empty (each then RLP-encodes as 0x80, rlp/encode.go:545-581).
+ * hash32_out (optional): CollationHeader.Hash() of the header as given (signature included).
+ * signer20_out (optional): crypto.Ecrecover(Hash() with ProposerSignature empty — the hash the
+ * proposer signs at sharding/proposer/proposer.go:83 — , sig) -> address, zero on failure.
+ * status: GSV_ST_OK when the signer equals ProposerAddress, GSV_ST_PROPOSER_MISMATCH when not,
+ * else the recovery status (GSV_ST_INVALID_RECID / GSV_ST_RECOVER_FAILED). */
+int gsv_collation_header_verify_batch(gsv_ctx *ctx, const uint8_t *shard_id32, const uint8_t *chunk_root32,
+                                      const uint8_t *period32, const uint8_t *proposer20, const uint8_t *sig65,
+                                      const uint8_t *nil_flags, size_t n, uint8_t *hash32_out,
+                                      uint8_t *signer20_out, uint8_t *status);
 
 #ifdef __cplusplus
 }

@@ -159,6 +159,76 @@ def trie_root(pairs) -> bytes:
     return out.raw
 
 
+def rlp_uint(i: int) -> bytes:
+    """rlp/encode.go:390 writeUint: 0 -> 0x80, < 128 -> the byte, else 0x80+len || big-endian."""
+    if i == 0:
+        return b"\x80"
+    if i < 128:
+        return bytes([i])
+    b = i.to_bytes((i.bit_length() + 7) // 8, "big")
+    return bytes([0x80 + len(b)]) + b
+
+
+def rlp_string(b: bytes) -> bytes:
+    """rlp/encode.go:71-89 encodeString"""
+    b = bytes(b)
+    if len(b) == 1 and b[0] < 0x80:
+        return b
+    if len(b) < 56:
+        return bytes([0x80 + len(b)]) + b
+    lb = len(b).to_bytes((len(b).bit_length() + 7) // 8, "big")
+    return bytes([0xb7 + len(lb)]) + lb + b
+
+
+def rlp_list(payload: bytes) -> bytes:
+    if len(payload) < 56:
+        return bytes([0xc0 + len(payload)]) + payload
+    lb = len(payload).to_bytes((len(payload).bit_length() + 7) // 8, "big")
+    return bytes([0xf7 + len(lb)]) + lb + payload
+
+
+def derive_sha(items) -> bytes:
+    """core/types/derive_sha.go:32-41: trie of (rlp(uint(j)), GetRlp(j)) -> root (restated trie)."""
+    if len(items) == 0:
+        return bytes.fromhex("56e81f171bcc55a6ff8345e692c0f86e5b48e01b996cadc001622fb5e363b421")
+    return trie_root([(rlp_uint(j), bytes(v)) for j, v in enumerate(items)])
+
+
+def calculate_poc(body: bytes, salt: bytes) -> bytes:
+    """sharding/collation.go:124-136: chunk root of salt||b0||salt||b1||... (salt for an empty body)."""
+    body, salt = bytes(body), bytes(salt)
+    if len(body) == 0:
+        salted = salt
+    else:
+        a = np.frombuffer(body, np.uint8)
+        m = np.empty((len(body), len(salt) + 1), np.uint8)
+        m[:, :len(salt)] = np.frombuffer(salt, np.uint8)
+        m[:, len(salt)] = a
+        salted = m.tobytes()
+    return derive_sha_bytes(salted)
+
+
+def _rlp_bigint(x) -> bytes:
+    x = 0 if x is None else int(x)
+    return b"\x80" if x == 0 else rlp_string(x.to_bytes((x.bit_length() + 7) // 8, "big"))
+
+
+def collation_header_rlp(shard_id, chunk_root, period, proposer, sig) -> bytes:
+    """rlp(collationHeaderData) (sharding/collation.go:35-43; nil pointers/slices -> 0x80,
+    rlp/encode.go:545-581)."""
+    f = [_rlp_bigint(shard_id),
+         b"\x80" if chunk_root is None else rlp_string(chunk_root),
+         _rlp_bigint(period),
+         b"\x80" if proposer is None else rlp_string(proposer),
+         rlp_string(sig or b"")]
+    return rlp_list(b"".join(f))
+
+
+def collation_header_hash(shard_id, chunk_root, period, proposer, sig) -> bytes:
+    """CollationHeader.Hash (sharding/collation.go:66-71)."""
+    return keccak256(collation_header_rlp(shard_id, chunk_root, period, proposer, sig))
+
+
 def secp_pubkey(seckey: bytes) -> bytes:
     out = ctypes.create_string_buffer(65)
     assert lib().oracle_secp_pubkey(out, seckey) == 1

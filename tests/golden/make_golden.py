@@ -320,8 +320,75 @@ def bn256_fixtures():
     dump("bn256.json", {"pairing": ref, "scalar_mul": smul, "generated": gen})
 
 
+def collation_fixtures():
+    """§8f rows 2-3: generic DeriveSha lists, Proof of Custody, collation header hash / signature."""
+    rng = random.Random(11)
+    # DeriveSha over lists of arbitrary values (tx-root shaped): sizes around the trie edge cases,
+    # items 1..300 bytes incl. single bytes < 0x80 (inline leaves) and >= 56 bytes (long strings)
+    derive = []
+    for n in [1, 2, 3, 16, 17, 127, 128, 129, 200, 256, 257, 1000]:
+        items = []
+        for j in range(n):
+            k = rng.choice([1, 1, 2, 20, 55, 56, 110, 300])
+            items.append(bytes(rng.getrandbits(8) for _ in range(k)))
+        derive.append({"items": [h(x) for x in items], "root": h(O.derive_sha(items))})
+    # Proof of Custody (sharding/collation.go:124-136)
+    poc = [{"body": "56ff", "salt": "019f", "source": "sharding/collation_test.go:132-149 inputs",
+            "poc": h(O.calculate_poc(bytes.fromhex("56ff"), bytes.fromhex("019f"))),
+            "chunk_root": h(O.derive_sha_bytes(bytes.fromhex("56ff")))}]
+    salt20 = bytes(rng.getrandbits(8) for _ in range(20))
+    poc.append({"body": "", "salt": h(salt20), "poc": h(O.calculate_poc(b"", salt20))})
+    b300 = bytes(rng.getrandbits(8) for _ in range(300))
+    poc.append({"body": h(b300), "salt": h(salt20), "source": "sharding/collation_test.go:312-324 shape",
+                "poc": h(O.calculate_poc(b300, salt20))})
+    b4k = bytes(rng.getrandbits(8) for _ in range(4096))
+    poc.append({"body": h(b4k), "salt": "0102", "poc": h(O.calculate_poc(b4k, b"\x01\x02"))})
+    poc.append({"body": h(b4k[:1000]), "salt": "", "poc": h(O.calculate_poc(b4k[:1000], b""))})
+    # > 2^24 salted leaves: 5-byte trie keys (rlp(uint) 0x84 ...)
+    big = xoshiro_bytes(11, 600000)
+    salt31 = bytes(range(31))
+    poc.append({"body": None, "xoshiro_seed": 11, "n": 600000, "salt": h(salt31),
+                "poc": h(O.calculate_poc(big, salt31))})
+    # collation headers: RLP/hash known answers + proposer signatures (oracle signer)
+    hdr = []
+
+    def add(sid, root, per, prop, sig, note):
+        hdr.append({"shard_id": sid, "chunk_root": None if root is None else h(root), "period": per,
+                    "proposer": None if prop is None else h(prop), "sig": None if sig is None else h(sig),
+                    "rlp": h(O.collation_header_rlp(sid, root, per, prop, sig)),
+                    "hash": h(O.collation_header_hash(sid, root, per, prop, sig)), "note": note})
+    add(1, None, 1, None, b"", "sharding/collation_test.go:133 NewCollationHeader(1, nil, 1, nil, []byte{})")
+    add(0, None, 0, None, None, "all zero / nil")
+    add(127, bytes(32), 128, bytes(20), None, "single-byte ints at the 0x7f/0x80 edge")
+    add(2**255 + 12345, bytes(range(32)), 2**64, bytes(range(20)), None, "wide big.Ints")
+    signed = []
+    for i in range(24):
+        key = (int.from_bytes(O.keccak256(b"gsv-hdr-key" + i.to_bytes(8, "little")), "big") % (N_ORDER - 1) + 1)
+        key = key.to_bytes(32, "big")
+        addr = O.keccak256(O.secp_pubkey(key)[1:])[12:]
+        sid, per = i % 100, 1000 + i
+        root = O.keccak256(b"gsv-hdr-root" + bytes([i]))
+        expect = "ok"
+        if i % 6 == 5:  # header claims someone else's address but is signed with this key
+            addr = O.keccak256(b"other" + bytes([i]))[12:]
+            expect = "mismatch"
+        msg = O.collation_header_hash(sid, root, per, addr, None)
+        sig = O.secp_sign(msg, key, O.keccak256(b"gsv-hdr-nonce" + bytes([i])))
+        if i % 6 == 4:  # recovery id out of range
+            sig = sig[:64] + bytes([4])
+            expect = "invalid_recid"
+        elif i % 6 == 3:  # r = 0
+            sig = bytes(32) + sig[32:]
+            expect = "recover_failed"
+        signed.append({"shard_id": sid, "chunk_root": h(root), "period": per, "proposer": h(addr), "sig": h(sig),
+                       "signer": h(O.keccak256(O.secp_pubkey(key)[1:])[12:]), "expect": expect,
+                       "hash": h(O.collation_header_hash(sid, root, per, addr, sig))})
+    dump("collation.json", {"derive_sha": derive, "poc": poc, "header_kat": hdr, "signed_headers": signed})
+
+
 FIXTURES = {"keccak": keccak_fixtures, "ecrecover": ecrecover_fixtures, "tx": tx_fixtures,
-            "trie": trie_fixtures, "chunk_root": chunk_root_fixtures, "bn256": bn256_fixtures}
+            "trie": trie_fixtures, "chunk_root": chunk_root_fixtures, "bn256": bn256_fixtures,
+            "collation": collation_fixtures}
 
 if __name__ == "__main__":
     if not O.ref_available():

@@ -196,3 +196,71 @@ def test_bn256_algorithmic_work_figure(oracle):
     import bench
     g = next(x for x in golden("bn256.json")["generated"] if x["note"] == "4-pair bilinear identity (true)")
     assert oracle.bn256_fp_muls(bytes.fromhex(g["input"])) == bench.FP_MULS_PER_CHECK
+
+
+# ---------------------------------------------------------------- §8f rows 2-3: DeriveSha, POC, headers
+def test_generic_derive_sha_pinned(oracle):
+    # core/types/block_test.go:29: TxHash = DeriveSha([tx]) — the generic-list restatement
+    for c in golden("trie.json")["derive_sha"]:
+        assert oracle.derive_sha([bytes.fromhex(x) for x in c["items"]]).hex() == c["root"]
+    assert oracle.derive_sha([]).hex() == golden("trie.json")["empty_root"]
+
+
+def test_generic_derive_sha_equals_chunk_root_restatement(oracle):
+    # two independent restatements: the generic (key, value) trie over Chunks.GetRlp(j) and the
+    # byte-body DeriveSha (sharding/collation.go:210-219)
+    rng = random.Random(5)
+    for n in [1, 2, 16, 17, 129, 300, 1000]:
+        body = bytes(rng.getrandbits(8) for _ in range(n))
+        # rlp(uint(byte)): 0 -> 0x80, < 128 -> byte, else 0x81 byte
+        items = [b"\x80" if b == 0 else bytes([b]) if b < 128 else bytes([0x81, b]) for b in body]
+        assert oracle.derive_sha(items) == oracle.derive_sha_bytes(body)
+
+
+def test_collation_fixtures_consistent(oracle):
+    g = golden("collation.json")
+    for c in g["derive_sha"]:
+        assert oracle.derive_sha([bytes.fromhex(x) for x in c["items"]]).hex() == c["root"]
+    for c in g["poc"]:
+        if c["body"] is None:
+            continue
+        assert oracle.calculate_poc(bytes.fromhex(c["body"]), bytes.fromhex(c["salt"])).hex() == c["poc"]
+    for c in g["header_kat"]:
+        root = None if c["chunk_root"] is None else bytes.fromhex(c["chunk_root"])
+        prop = None if c["proposer"] is None else bytes.fromhex(c["proposer"])
+        sig = None if c["sig"] is None else bytes.fromhex(c["sig"])
+        rlp = oracle.collation_header_rlp(c["shard_id"], root, c["period"], prop, sig)
+        assert rlp.hex() == c["rlp"]
+        assert oracle.keccak256(rlp).hex() == c["hash"]
+    for c in g["signed_headers"]:
+        root, prop, sig = (bytes.fromhex(c[k]) for k in ("chunk_root", "proposer", "sig"))
+        assert oracle.collation_header_hash(c["shard_id"], root, c["period"], prop, sig).hex() == c["hash"]
+        msg = oracle.collation_header_hash(c["shard_id"], root, c["period"], prop, None)
+        if c["expect"] in ("ok", "mismatch"):
+            rc, pub = oracle.ecrecover(msg, sig)
+            assert rc == 1
+            signer = oracle.keccak256(pub[1:])[12:]
+            assert signer.hex() == c["signer"]
+            assert (signer == prop) == (c["expect"] == "ok")
+
+
+def test_poc_reference_properties(oracle):
+    # sharding/collation_test.go:132-149: the POC with salt differs from the chunk root
+    c = golden("collation.json")["poc"][0]
+    assert c["poc"] != c["chunk_root"]
+    # empty body: the salt alone is chunked (sharding/collation.go:131-133)
+    salt = bytes(range(20))
+    assert oracle.calculate_poc(b"", salt) == oracle.derive_sha_bytes(salt)
+    # empty salt: the POC is the chunk root
+    assert oracle.calculate_poc(b"\x01\x02\x03", b"") == oracle.derive_sha_bytes(b"\x01\x02\x03")
+
+
+def test_collation_header_rlp_rules(oracle):
+    # NewCollationHeader(big 1, nil, big 1, nil, []byte{}) (sharding/collation_test.go:133):
+    # big.Int 1 -> 0x01, nil *common.Hash / *common.Address -> 0x80 (rlp/encode.go:555-559),
+    # empty []byte -> 0x80; list of 5 bytes -> 0xc5
+    assert oracle.collation_header_rlp(1, None, 1, None, b"").hex() == "c50180018080"
+    # big.Int 0 -> 0x80 (rlp/encode.go:433), 128 -> 81 80, 32-byte hash -> a0 ..., 65-byte sig -> b8 41 ...
+    r = oracle.collation_header_rlp(0, bytes(32), 128, bytes(20), bytes(65))
+    assert r[:4].hex() == "f8" + "%02x" % (len(r) - 2) + "80a0"
+    assert r[-67:-65].hex() == "b841"
