@@ -7,8 +7,9 @@
 // the same length in one launch per level:
 //   kind BOTTOM  a full branch whose 16 children are leaves [0x20, rlp(byte)] -> 1 permutation,
 //                built from 16 body bytes (the bulk: N/16 nodes);
-//   kind HFULL   a full branch whose 16 children are all hashed -> 532-byte message, 4 permutations,
-//                children write their "a0 || hash" straight into its message buffer;
+//   kind HFULL   a full branch whose 16 children are all hashed -> 532-byte message, 4 permutations;
+//                children store their raw 32-byte hashes (aligned) into its buffer and the message
+//                f9 02 11 | (a0 || H_s) x 16 | 80 is generated word by word at compile-time offsets;
 //   kind BRANCH / EXT / LEAF  generic nodes (partial right edge, top of trie, root): assembled
 //                byte by byte from children refs, inlined when RLP < 32 bytes (trie/hasher.go:163),
 //                the root always hashed (force).
@@ -36,7 +37,7 @@ struct PNode {
     uint8_t is_root;
     uint8_t nchild;       // generic: number of child entries
     int32_t msg_off;      // own message buffer offset in the per-body msg arena (-1 for BOTTOM)
-    int32_t parent_msg;   // byte offset in the arena where this node's 33-byte ref goes (HFULL parent), or -1
+    int32_t parent_msg;   // HFULL parent: byte offset in the msg arena of this node's 32-byte hash slot, or -1
     int32_t ref_slot;     // canonical ref slot (generic parents read refs from here)
     uint32_t first_i;     // BOTTOM: body index of child 0; LEAF: body index
     int32_t child_begin;  // generic: first entry in the child array
@@ -51,7 +52,11 @@ struct PChild {
     uint32_t idx;    // leaf: body index; node: node id
 };
 
-constexpr int MSG_STRIDE = 544;  // bytes per message buffer (532 max + padding to the 4th block end)
+constexpr int MSG_STRIDE = 544;  // bytes per message buffer (532 max + padding to the 4th block end);
+                                 // an HFULL node's buffer holds its 16 children's raw hashes (512 B)
+constexpr int TOP_MAX_HFULL = 1024;  // fused-top eligibility per height (per body)
+constexpr int TOP_MAX_GEN = 64;
+constexpr int TOP_MAX_H = 24;
 constexpr int REF_STRIDE = 48;   // bytes per ref slot: [0] = length, [8..41) = ref bytes
 
 struct TriePlanHost {
@@ -61,8 +66,9 @@ struct TriePlanHost {
     std::vector<PNode> nodes;     // sorted by height, BOTTOM first inside height 1
     std::vector<PChild> children;
     // per height h (1..H): [bottom_begin, bottom_end) and [gen_begin, gen_end) node id ranges
-    std::vector<int> lvl_bottom_begin, lvl_bottom_end, lvl_gen_begin, lvl_gen_end;
+    std::vector<int> lvl_bottom_begin, lvl_bottom_end, lvl_hfull_begin, lvl_hfull_end, lvl_gen_begin, lvl_gen_end;
     int height = 0;
+    int top_h = 1;  // heights top_h..height run fused in k_chunk_top (one workgroup per body)
     int root = -1;
     int n_msg = 0;    // message buffers per body
     int n_slots = 0;  // ref slots per body

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <utility>
 
 #include "chunk_root.h"
 #include "gsv_internal.h"
@@ -174,14 +175,15 @@ void build_trie_plan(TriePlanHost& p, uint32_t N, bool generic) {
     }
     b.nodes[root].is_root = 1;
     // an HFULL root still has to produce the root hash (no parent message): fine, handled in-kernel
-    // order: by height, BOTTOM first at height 1
+    // order: by height; inside a height BOTTOM, then HFULL, then generic nodes
     int M = (int)b.nodes.size();
     std::vector<int> order(M);
     for (int i = 0; i < M; i++) order[i] = i;
+    auto rank = [](uint8_t k) { return k == PK_BOTTOM ? 0 : k == PK_HFULL ? 1 : 2; };
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
         const PNode &a = b.nodes[x], &c = b.nodes[y];
         if (a.height != c.height) return a.height < c.height;
-        return (a.kind == PK_BOTTOM) > (c.kind == PK_BOTTOM);
+        return rank(a.kind) < rank(c.kind);
     });
     std::vector<int> newid(M);
     for (int i = 0; i < M; i++) newid[order[i]] = i;
@@ -203,32 +205,39 @@ void build_trie_plan(TriePlanHost& p, uint32_t N, bool generic) {
         }
         p.nodes[i] = n;
     }
-    // HFULL parents: children write "a0 || hash" at 3 + 33 * slot of the parent's message
+    // HFULL parents: children store their raw 32-byte hash at 32 * slot of the parent's buffer
     for (int i = 0; i < M; i++) {
         int o = order[i];
         if (b.nodes[o].kind != PK_HFULL) continue;
-        for (auto& c : b.kids[o]) p.nodes[newid[c.idx]].parent_msg = p.nodes[i].msg_off + 3 + 33 * c.slot;
+        for (auto& c : b.kids[o]) p.nodes[newid[c.idx]].parent_msg = p.nodes[i].msg_off + 32 * c.slot;
     }
     p.root = newid[root];
     p.n_msg = nmsg;
     p.n_slots = M;
     p.height = p.nodes.back().height;
-    for (int h = 1; h <= p.height; h++) {
-        int bb = -1, be = -1, gb = -1, ge = -1;
-        for (int i = 0; i < M; i++) {
-            if (p.nodes[i].height != h) continue;
-            if (p.nodes[i].kind == PK_BOTTOM) {
-                if (bb < 0) bb = i;
-                be = i + 1;
-            } else {
-                if (gb < 0) gb = i;
-                ge = i + 1;
-            }
-        }
-        p.lvl_bottom_begin.push_back(bb < 0 ? 0 : bb);
-        p.lvl_bottom_end.push_back(bb < 0 ? 0 : be);
-        p.lvl_gen_begin.push_back(gb < 0 ? 0 : gb);
-        p.lvl_gen_end.push_back(gb < 0 ? 0 : ge);
+    p.lvl_bottom_begin.assign(p.height, 0);
+    p.lvl_bottom_end.assign(p.height, 0);
+    p.lvl_hfull_begin.assign(p.height, 0);
+    p.lvl_hfull_end.assign(p.height, 0);
+    p.lvl_gen_begin.assign(p.height, 0);
+    p.lvl_gen_end.assign(p.height, 0);
+    for (int i = M - 1; i >= 0; i--) {  // nodes are sorted: the first index seen last wins
+        int h = p.nodes[i].height - 1;
+        uint8_t k = p.nodes[i].kind;
+        std::vector<int>& bg = k == PK_BOTTOM ? p.lvl_bottom_begin : k == PK_HFULL ? p.lvl_hfull_begin : p.lvl_gen_begin;
+        std::vector<int>& en = k == PK_BOTTOM ? p.lvl_bottom_end : k == PK_HFULL ? p.lvl_hfull_end : p.lvl_gen_end;
+        if (en[h] == 0) en[h] = i + 1;
+        bg[h] = i;
+    }
+    // the top of the trie (few nodes per height, no BOTTOM) runs as one fused launch: one
+    // workgroup per body walks those heights with barriers instead of one launch per height
+    p.top_h = p.height + 1;
+    for (int h = p.height; h >= 1; h--) {
+        int nb = p.lvl_bottom_end[h - 1] - p.lvl_bottom_begin[h - 1];
+        int nf = p.lvl_hfull_end[h - 1] - p.lvl_hfull_begin[h - 1];
+        int ng = p.lvl_gen_end[h - 1] - p.lvl_gen_begin[h - 1];
+        if (nb || nf > TOP_MAX_HFULL || ng > TOP_MAX_GEN) break;
+        p.top_h = h;
     }
 }
 
@@ -285,7 +294,7 @@ struct BodyBatch {
     int generic;
 };
 
-// Keccak-256 of len bytes at p (8-byte aligned; bytes past len may be garbage)
+// Keccak-256 of len bytes at p (8-byte aligned, global or LDS; bytes past len may be garbage)
 GSV_DI void keccak_buf(uint32_t h[8], const uint8_t* p, uint32_t len) {
     uint64_t a[25];
 #pragma unroll
@@ -316,29 +325,37 @@ GSV_DI void keccak_buf(uint32_t h[8], const uint8_t* p, uint32_t len) {
     }
 }
 
-// write "a0 || hash" (33 bytes) at dst, byte granular
-GSV_DI void put_hashref(uint8_t* dst, const uint32_t h[8]) {
-    dst[0] = 0xa0;
-#pragma unroll
-    for (int w = 0; w < 8; w++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) dst[1 + 4 * w + b] = (uint8_t)(h[w] >> (8 * b));
+// raw 32-byte hash to a 16-byte aligned destination (two dwordx4 stores)
+GSV_DI void store_hash32(uint8_t* dst, const uint32_t h[8]) {
+    uint4* d = (uint4*)dst;
+    d[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    d[1] = make_uint4(h[4], h[5], h[6], h[7]);
 }
 
-// deliver a hashed node's reference (root output / parent message / canonical slot)
+// canonical ref slot (16-byte aligned): s[0] = 33, s[8 .. 41) = a0 || hash
+GSV_DI void store_hashref_slot(uint8_t* s, const uint32_t h[8]) {
+    uint32_t w[12];
+    w[0] = 33;
+    w[1] = 0;
+    w[2] = 0xa0u | (h[0] << 8);
+#pragma unroll
+    for (int k = 1; k < 8; k++) w[2 + k] = (h[k - 1] >> 24) | (h[k] << 8);
+    w[10] = h[7] >> 24;
+    w[11] = 0;
+    uint4* d = (uint4*)s;
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    d[2] = make_uint4(w[8], w[9], w[10], w[11]);
+}
+
+// deliver a hashed node's reference (root output / HFULL parent's hash slot / canonical slot)
 GSV_DI void emit_hash(const PNode& nd, const BodyBatch& bb, uint32_t body, const uint32_t h[8]) {
     if (nd.is_root) {
-        uint8_t* o = bb.roots + (size_t)body * 32;
-#pragma unroll
-        for (int w = 0; w < 8; w++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) o[4 * w + b] = (uint8_t)(h[w] >> (8 * b));
+        store_hash32(bb.roots + (size_t)body * 32, h);
     } else if (nd.parent_msg >= 0) {
-        put_hashref(bb.msg + (size_t)body * bb.msg_stride + nd.parent_msg, h);
+        store_hash32(bb.msg + (size_t)body * bb.msg_stride + nd.parent_msg, h);
     } else {
-        uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE;
-        s[0] = 33;
-        put_hashref(s + 8, h);
+        store_hashref_slot(bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE, h);
     }
 }
 
@@ -347,14 +364,8 @@ GSV_DI void emit_hash(const PNode& nd, const BodyBatch& bb, uint32_t body, const
 constexpr int BOT_BLOCK = 256;
 constexpr int BOT_BUF = 96;
 
-__global__ __launch_bounds__(BOT_BLOCK) void k_chunk_bottom(const PNode* __restrict__ nodes, int nb0,
-                                                            int ncount, BodyBatch bb) {
-    __shared__ uint64_t sbuf64[BOT_BLOCK * BOT_BUF / 8];
-    uint64_t t = (uint64_t)blockIdx.x * BOT_BLOCK + threadIdx.x;
-    if (t >= (uint64_t)ncount * bb.nbodies) return;
-    uint32_t body = (uint32_t)(t / (uint64_t)ncount);
-    int ni = nb0 + (int)(t % (uint64_t)ncount);
-    const PNode nd = nodes[ni];
+// m: this lane's BOT_BUF-byte LDS buffer (8-byte aligned)
+GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8_t* m) {
     const uint8_t* src = bb.bodies + bb.body_off[body] + nd.first_i;
     uint8_t v[16];
     if ((((uintptr_t)src) & 15u) == 0) {
@@ -369,7 +380,6 @@ __global__ __launch_bounds__(BOT_BLOCK) void k_chunk_bottom(const PNode* __restr
     uint32_t payload = 1;  // trailing empty value slot 0x80
 #pragma unroll
     for (int j = 0; j < 16; j++) payload += v[j] == 0 ? 4u : v[j] < 128 ? 3u : 5u;
-    uint8_t* m = (uint8_t*)sbuf64 + threadIdx.x * BOT_BUF;
     uint32_t o = 0;
     if (payload < 56) {
         m[o++] = (uint8_t)(0xc0 + payload);
@@ -416,7 +426,81 @@ __global__ __launch_bounds__(BOT_BLOCK) void k_chunk_bottom(const PNode* __restr
     emit_hash(nd, bb, body, h);
 }
 
-// ---------------------------------------------------------------- generic encoding helpers
+// ---------------------------------------------------------------- HFULL: 16 hashed children
+constexpr int HF_LEN = 532;
+constexpr bool hf_is_const(int p) { return p < 3 || p >= HF_LEN - 1 || (p - 3) % 33 == 0; }
+constexpr uint32_t hf_const(int p) {
+    return p == 0 ? 0xf9u : p == 1 ? 0x02u : p == 2 ? 0x11u : p == HF_LEN - 1 ? 0x80u : p >= HF_LEN ? 0u : 0xa0u;
+}
+constexpr int hf_slot(int p) { return (p - 3) / 33; }
+constexpr int hf_idx(int p) { return (p - 3) % 33 - 1; }
+// child-hash slots touched by block B (136 bytes at 136 * B)
+constexpr int hf_s0(int B) { return B == 0 ? 0 : hf_slot(136 * B); }
+constexpr int hf_s1(int B) { return hf_slot(136 * B + 135 < HF_LEN - 2 ? 136 * B + 135 : HF_LEN - 2); }
+
+template <int B, int P>
+GSV_DI uint32_t hf_byte(const uint32_t* win) {
+    constexpr int p = 136 * B + P;
+    if constexpr (hf_is_const(p)) {
+        return hf_const(p);
+    } else {
+        constexpr int s = hf_slot(p) - hf_s0(B), j = hf_idx(p);
+        return (win[s * 8 + (j >> 2)] >> (8 * (j & 3))) & 0xffu;
+    }
+}
+template <int B, int W>
+GSV_DI uint32_t hf_word(const uint32_t* win) {
+    return hf_byte<B, 4 * W>(win) | (hf_byte<B, 4 * W + 1>(win) << 8) | (hf_byte<B, 4 * W + 2>(win) << 16) |
+           (hf_byte<B, 4 * W + 3>(win) << 24);
+}
+template <int B, int... K>
+GSV_DI void hf_absorb(uint32_t al[25], uint32_t ah[25], const uint32_t* win, std::integer_sequence<int, K...>) {
+    ((al[K] ^= hf_word<B, 2 * K>(win), ah[K] ^= hf_word<B, 2 * K + 1>(win)), ...);
+}
+template <int B>
+GSV_DI void hf_block(uint32_t al[25], uint32_t ah[25], const uint4* __restrict__ Hq) {
+    constexpr int s0 = hf_s0(B), ns = hf_s1(B) - s0 + 1;
+    uint32_t win[ns * 8];
+#pragma unroll
+    for (int s = 0; s < ns; s++) {
+        uint4 a = Hq[2 * (s0 + s)], b = Hq[2 * (s0 + s) + 1];
+        win[8 * s + 0] = a.x; win[8 * s + 1] = a.y; win[8 * s + 2] = a.z; win[8 * s + 3] = a.w;
+        win[8 * s + 4] = b.x; win[8 * s + 5] = b.y; win[8 * s + 6] = b.z; win[8 * s + 7] = b.w;
+    }
+    hf_absorb<B>(al, ah, win, std::make_integer_sequence<int, 17>{});
+    if constexpr (B == 3) {  // pad: 0x01 at byte 532 - 408 = 124 (lane 15, high half), 0x80 at byte 135
+        ah[15] ^= 0x01u;
+        ah[16] ^= 0x80000000u;
+    }
+    keccakf_split(al, ah);
+}
+// Keccak-256 of the full branch f9 02 11 | (a0 || H_0) ... (a0 || H_15) | 80 (532 bytes, 4 blocks).
+// Every byte's source is a compile-time function of its offset (templates above), so each 32-bit
+// message word is a shift/or of at most two child-hash words held in registers — no message buffer.
+GSV_DI void hash_hfull(uint32_t h[8], const uint32_t* __restrict__ H) {
+    uint32_t al[25], ah[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) al[k] = ah[k] = 0;
+    const uint4* Hq = (const uint4*)H;
+    hf_block<0>(al, ah, Hq);
+    hf_block<1>(al, ah, Hq);
+    hf_block<2>(al, ah, Hq);
+    hf_block<3>(al, ah, Hq);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        h[2 * k] = al[k];
+        h[2 * k + 1] = ah[k];
+    }
+}
+
+GSV_DI void do_hfull(const PNode& nd, const BodyBatch& bb, uint32_t body) {
+    const uint32_t* H = (const uint32_t*)(bb.msg + (size_t)body * bb.msg_stride + nd.msg_off);
+    uint32_t h[8];
+    hash_hfull(h, H);
+    emit_hash(nd, bb, body, h);
+}
+
+// ---------------------------------------------------------------- generic nodes
 // compact encoding (trie/encoding.go:37-52) of nibbles key(i)[d0:d1] (terminator included iff
 // present); returns byte length, writes into c[0..]
 GSV_DI int compact_key(uint8_t c[8], uint32_t i, int d0, int d1) {
@@ -437,17 +521,13 @@ GSV_DI int compact_key(uint8_t c[8], uint32_t i, int d0, int d1) {
 struct Writer {
     uint8_t* p;
     uint32_t n;
-    bool dry;
-    GSV_DI void put(uint8_t b) {
-        if (!dry) p[n] = b;
-        n++;
-    }
-    GSV_DI void str(const uint8_t* s, int len) {  // RLP string
+    GSV_DI void put(uint8_t b) { p[n++] = b; }
+    GSV_DI void str(const uint8_t* s, int len) {  // RLP string, len < 56
         if (len == 1 && s[0] < 0x80) {
             put(s[0]);
             return;
         }
-        put((uint8_t)(0x80 + len));  // len < 56 here
+        put((uint8_t)(0x80 + len));
         for (int k = 0; k < len; k++) put(s[k]);
     }
     GSV_DI void list_header(uint32_t len) {
@@ -463,14 +543,9 @@ struct Writer {
     }
 };
 
-// leaf [compact(rem), rlp(value)] where value = rlp(uint(body byte))
-GSV_DI void write_leaf(Writer& w, uint32_t i, int d, uint8_t b) {
-    uint8_t ck[8];
-    int cl = compact_key(ck, i, d, key_len(i));
-    uint32_t klen = (cl == 1 && ck[0] < 0x80) ? 1u : 1u + cl;
-    uint32_t vlen = b == 0 ? 2u : b < 128 ? 1u : 3u;
-    w.list_header(klen + vlen);
-    w.str(ck, cl);
+GSV_DI uint32_t str_len(const uint8_t* s, int len) { return (len == 1 && s[0] < 0x80) ? 1u : 1u + len; }
+GSV_DI uint32_t byte_val_len(uint8_t b) { return b == 0 ? 2u : b < 128 ? 1u : 3u; }  // rlp(rlp(uint(b)))
+GSV_DI void put_byte_val(Writer& w, uint8_t b) {
     if (b == 0) {
         w.put(0x81);
         w.put(0x80);
@@ -483,95 +558,170 @@ GSV_DI void write_leaf(Writer& w, uint32_t i, int d, uint8_t b) {
     }
 }
 
-GSV_DI void write_child_ref(Writer& w, const BodyBatch& bb, uint32_t body, const PChild& c,
-                            const PNode* nodes) {
-    if (c.type == PC_LEAF && bb.generic) {
-        const uint8_t* s = bb.leafrefs + (bb.leaf_base[body] + c.idx) * REF_STRIDE;
-        uint32_t len = s[0];
-        for (uint32_t k = 0; k < len; k++) w.put(s[8 + k]);
-    } else if (c.type == PC_LEAF) {
-        uint8_t b = bb.bodies[bb.body_off[body] + c.idx];
-        write_leaf(w, c.idx, c.depth, b);
-    } else {
-        const uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nodes[c.idx].ref_slot * REF_STRIDE;
-        uint32_t len = s[0];
-        for (uint32_t k = 0; k < len; k++) w.put(s[8 + k]);
-    }
+// byte-mode leaf [compact(rem), rlp(value)] where value = rlp(uint(body byte)): RLP length
+GSV_DI uint32_t leaf_len(uint32_t i, int d, uint8_t b) {
+    uint8_t ck[8];
+    int cl = compact_key(ck, i, d, key_len(i));
+    uint32_t pl = str_len(ck, cl) + byte_val_len(b);
+    return pl + 1;  // pl < 56
+}
+GSV_DI void write_leaf(Writer& w, uint32_t i, int d, uint8_t b) {
+    uint8_t ck[8];
+    int cl = compact_key(ck, i, d, key_len(i));
+    w.list_header(str_len(ck, cl) + byte_val_len(b));
+    w.str(ck, cl);
+    put_byte_val(w, b);
 }
 
-// payload of a generic node into w
-GSV_DI void write_payload(Writer& w, const PNode& nd, const PChild* ch, const BodyBatch& bb,
-                          uint32_t body, const PNode* nodes) {
+// ref slot (16-byte aligned, global) -> its bytes appended to w; returns its length
+GSV_DI void copy_ref(Writer& w, const uint8_t* s) {
+    const uint4* q = (const uint4*)s;
+    uint4 a = q[0], b = q[1], c = q[2];
+    uint32_t x[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+    uint32_t len = x[0] & 0xffu;
+#pragma unroll
+    for (int k = 0; k < 33; k++)
+        if ((uint32_t)k < len) w.put((uint8_t)(x[(k + 8) >> 2] >> (8 * ((k + 8) & 3))));
+}
+GSV_DI uint32_t ref_len(const uint8_t* s) { return s[0]; }
+
+GSV_DI const uint8_t* child_slot(const BodyBatch& bb, uint32_t body, const PChild& c, const PNode* nodes) {
+    if (c.type == PC_LEAF) return bb.leafrefs + (bb.leaf_base[body] + c.idx) * REF_STRIDE;
+    return bb.refs + (size_t)body * bb.ref_stride + (size_t)nodes[c.idx].ref_slot * REF_STRIDE;
+}
+GSV_DI uint32_t child_len(const BodyBatch& bb, uint32_t body, const PChild& c, const PNode* nodes) {
+    if (c.type == PC_LEAF && !bb.generic) return leaf_len(c.idx, c.depth, bb.bodies[bb.body_off[body] + c.idx]);
+    return ref_len(child_slot(bb, body, c, nodes));
+}
+GSV_DI void write_child(Writer& w, const BodyBatch& bb, uint32_t body, const PChild& c, const PNode* nodes) {
+    if (c.type == PC_LEAF && !bb.generic) write_leaf(w, c.idx, c.depth, bb.bodies[bb.body_off[body] + c.idx]);
+    else copy_ref(w, child_slot(bb, body, c, nodes));
+}
+
+// One generic node (BRANCH / EXT / byte-mode root LEAF), assembled by a whole wave: lane k writes
+// piece k of the RLP payload (BRANCH: slots 0..15 + the value slot; EXT / LEAF: key, child/value)
+// at an offset from a wave prefix sum into the wave's LDS buffer m (8-byte aligned, MSG_STRIDE
+// bytes), so the ≤16 child-ref loads are issued in parallel; lane 0 then hashes (>= 32 bytes or
+// root, trie/hasher.go:163) or inlines the RLP into the node's ref slot.  All 64 lanes must call.
+GSV_DI void do_generic_wave(const PNode& nd, const PChild* __restrict__ children, const PNode* __restrict__ nodes,
+                            const BodyBatch& bb, uint32_t body, uint8_t* m) {
+    const int lane = threadIdx.x & 63;
+    const PChild* ch = nd.child_begin >= 0 ? children + nd.child_begin : nullptr;
+    // this lane's piece: 0 none, 1 empty slot / value slot (0x80), 2 child, 3 key, 4 byte value
+    int piece = 0;
+    const PChild* mine = nullptr;
+    uint8_t ck[8];
+    int cl = 0;
     if (nd.kind == PK_BRANCH) {
-        int k = 0;
-        for (int slot = 0; slot < 16; slot++) {
-            if (k < nd.nchild && ch[k].slot == slot) {
-                write_child_ref(w, bb, body, ch[k], nodes);
-                k++;
-            } else {
-                w.put(0x80);
-            }
+        if (lane < 16) {
+            piece = 1;
+            for (int k = 0; k < nd.nchild; k++)
+                if (ch[k].slot == lane) {
+                    piece = 2;
+                    mine = ch + k;
+                }
+        } else if (lane == 16) {
+            piece = 1;  // value slot (never set: keys are prefix-free)
         }
-        w.put(0x80);  // value slot (never set: keys are prefix-free)
-    } else if (nd.kind == PK_EXT) {
-        uint8_t ck[8];
-        int cl = compact_key(ck, nd.first_i, nd.depth, nd.ext_end);
-        w.str(ck, cl);
-        write_child_ref(w, bb, body, ch[0], nodes);
-    } else {  // PK_LEAF (root of a 1-byte body)
-        uint8_t b = bb.bodies[bb.body_off[body] + nd.first_i];
-        uint8_t ck[8];
-        int cl = compact_key(ck, nd.first_i, nd.depth, key_len(nd.first_i));
-        w.str(ck, cl);
-        if (b == 0) {
-            w.put(0x81);
-            w.put(0x80);
-        } else if (b < 128) {
-            w.put(b);
+    } else if (lane == 0) {
+        piece = 3;
+        cl = nd.kind == PK_EXT ? compact_key(ck, nd.first_i, nd.depth, nd.ext_end)
+                               : compact_key(ck, nd.first_i, nd.depth, key_len(nd.first_i));
+    } else if (lane == 1) {
+        piece = nd.kind == PK_EXT ? 2 : 4;
+        mine = ch;
+    }
+    uint8_t bval = piece == 4 ? bb.bodies[bb.body_off[body] + nd.first_i] : 0;
+    uint32_t plen = piece == 1 ? 1u : piece == 2 ? child_len(bb, body, *mine, nodes)
+                  : piece == 3 ? str_len(ck, cl) : piece == 4 ? byte_val_len(bval) : 0u;
+    uint32_t incl = plen;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    uint32_t total = __shfl(incl, 63, 64);
+    uint32_t hl = total < 56 ? 1u : total < 256 ? 2u : 3u;
+    Writer w{m, hl + incl - plen};
+    if (piece == 1) w.put(0x80);
+    else if (piece == 2) write_child(w, bb, body, *mine, nodes);
+    else if (piece == 3) w.str(ck, cl);
+    else if (piece == 4) put_byte_val(w, bval);
+    if (lane == 0) {
+        Writer hw{m, 0};
+        hw.list_header(total);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t len = hl + total;
+    if (lane == 0) {
+        if (len >= 32 || nd.is_root) {
+            uint32_t h[8];
+            keccak_buf(h, m, len);
+            emit_hash(nd, bb, body, h);
         } else {
-            w.put(0x82);
-            w.put(0x81);
-            w.put(b);
+            uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE;
+            s[0] = (uint8_t)len;
+            for (uint32_t k = 0; k < len; k++) s[8 + k] = m[k];
         }
     }
 }
 
+// One height below the fused top: generic nodes (one wave each) in the first gen_blocks workgroups
+// so their latency-bound chains start first, then BOTTOM (height 1) or HFULL nodes one per lane in
+// the same launch (they are independent of each other within a height).
+struct LevelLaunch {
+    int n0, nn;  // BOTTOM (BOT) or HFULL (!BOT) node range
+    int g0, ng;  // generic node range
+    uint32_t gen_blocks;
+};
+template <bool BOT>
 __global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ nodes,
-                                                     const PChild* __restrict__ children, int g0,
-                                                     int ncount, BodyBatch bb) {
-    uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= (uint64_t)ncount * bb.nbodies) return;
-    uint32_t body = (uint32_t)(t / (uint64_t)ncount);
-    int ni = g0 + (int)(t % (uint64_t)ncount);
-    const PNode nd = nodes[ni];
-    uint8_t* m = bb.msg + (size_t)body * bb.msg_stride + nd.msg_off;
-    uint32_t h[8];
-    if (nd.kind == PK_HFULL) {
-        // children wrote bytes [3, 531); header f9 02 11, value slot 0x80 at 531
-        m[0] = 0xf9;
-        m[1] = 0x02;
-        m[2] = 0x11;
-        m[531] = 0x80;
-        keccak_buf(h, m, 532);
-        emit_hash(nd, bb, body, h);
+                                                     const PChild* __restrict__ children, LevelLaunch L,
+                                                     BodyBatch bb) {
+    __shared__ uint64_t sbuf[(BOT ? 256 * BOT_BUF : 4 * MSG_STRIDE) / 8];
+    uint32_t blk = blockIdx.x;
+    if (blk < L.gen_blocks) {
+        uint64_t w = (uint64_t)blk * 4 + (threadIdx.x >> 6);
+        if (w >= (uint64_t)L.ng * bb.nbodies) return;  // uniform per wave
+        uint32_t body = (uint32_t)(w / (uint64_t)L.ng);
+        const PNode nd = nodes[L.g0 + (int)(w % (uint64_t)L.ng)];
+        do_generic_wave(nd, children, nodes, bb, body, (uint8_t*)sbuf + (threadIdx.x >> 6) * MSG_STRIDE);
         return;
     }
-    const PChild* ch = nd.child_begin >= 0 ? children + nd.child_begin : nullptr;
-    Writer dry{m, 0, true};
-    write_payload(dry, nd, ch, bb, body, nodes);
-    uint32_t plen = dry.n;
-    Writer w{m, 0, false};
-    w.list_header(plen);
-    write_payload(w, nd, ch, bb, body, nodes);
-    uint32_t len = w.n;
-    if (len >= 32 || nd.is_root) {
-        keccak_buf(h, m, len);
-        emit_hash(nd, bb, body, h);
-    } else {
-        // inline: the RLP itself is the reference (trie/hasher.go:163)
-        uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE;
-        s[0] = (uint8_t)len;
-        for (uint32_t k = 0; k < len; k++) s[8 + k] = m[k];
+    uint64_t t = (uint64_t)(blk - L.gen_blocks) * 256 + threadIdx.x;
+    if (t >= (uint64_t)L.nn * bb.nbodies) return;
+    uint32_t body = (uint32_t)(t / (uint64_t)L.nn);
+    const PNode nd = nodes[L.n0 + (int)(t % (uint64_t)L.nn)];
+    if constexpr (BOT) do_bottom(nd, bb, body, (uint8_t*)sbuf + threadIdx.x * BOT_BUF);
+    else do_hfull(nd, bb, body);
+}
+
+// ---------------------------------------------------------------- fused top of the trie
+struct TopLevels {
+    int h0, h1;  // heights h0..h1 (inclusive), index h - 1 below
+    int hb[TOP_MAX_H], he[TOP_MAX_H], gb[TOP_MAX_H], ge[TOP_MAX_H];
+};
+constexpr int TOP_BLOCK = 256;
+constexpr int TOP_WAVES = TOP_BLOCK / 64;
+
+// one workgroup per body; per height: HFULL nodes one per lane, generic nodes one per wave (LDS
+// message buffers), a barrier between heights (children's hashes are in the CU's L1/L2)
+__global__ __launch_bounds__(TOP_BLOCK) void k_chunk_top(const PNode* __restrict__ nodes,
+                                                         const PChild* __restrict__ children, TopLevels tl,
+                                                         BodyBatch bb) {
+    __shared__ uint64_t gbuf[TOP_WAVES * MSG_STRIDE / 8];
+    uint32_t body = blockIdx.x;
+    int tid = threadIdx.x, wave = tid >> 6;
+    uint8_t* m = (uint8_t*)gbuf + wave * MSG_STRIDE;
+    for (int h = tl.h0; h <= tl.h1; h++) {
+        int hb = tl.hb[h - 1], he = tl.he[h - 1];
+        for (int i = hb + tid; i < he; i += TOP_BLOCK) do_hfull(nodes[i], bb, body);
+        int gb = tl.gb[h - 1], ge = tl.ge[h - 1];
+        for (int i = gb + (TOP_WAVES - 1 - wave); i < ge; i += TOP_WAVES)
+            do_generic_wave(nodes[i], children, nodes, bb, body, m);
+        __syncthreads();
     }
 }
 
@@ -580,6 +730,56 @@ size_t chunk_root_scratch_bytes(const TriePlan* plan, uint32_t nbodies) {
     size_t ms = (size_t)plan->h.n_msg * MSG_STRIDE;
     size_t rs = (size_t)plan->h.n_slots * REF_STRIDE;
     return (ms + rs) * nbodies + 512;
+}
+
+// all heights of the plan: per-height launches below top_h, then one fused launch
+static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipStream_t st,
+                                void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx) {
+    const TriePlanHost& p = plan->h;
+    uint32_t nb = bb.nbodies;
+    for (int h = 1; h < p.top_h; h++) {
+        int b0 = p.lvl_bottom_begin[h - 1], b1 = p.lvl_bottom_end[h - 1];
+        int f0 = p.lvl_hfull_begin[h - 1], f1 = p.lvl_hfull_end[h - 1];
+        int g0 = p.lvl_gen_begin[h - 1], g1 = p.lvl_gen_end[h - 1];
+        bool bot = b1 > b0;  // BOTTOM nodes only exist at height 1, where there is no HFULL node
+        LevelLaunch L;
+        L.n0 = bot ? b0 : f0;
+        L.nn = bot ? b1 - b0 : f1 - f0;
+        L.g0 = g0;
+        L.ng = g1 - g0;
+        L.gen_blocks = (uint32_t)(((uint64_t)L.ng * nb + 3) / 4);
+        uint64_t blocks = L.gen_blocks + ((uint64_t)L.nn * nb + 255) / 256;
+        if (blocks == 0) continue;
+        int kid = bot ? GSV_K_CHUNK_LEAF : GSV_K_CHUNK_LEVEL;
+        if (timer_begin) timer_begin(tctx, kid);
+        if (bot)
+            hipLaunchKernelGGL(k_chunk_level<true>, dim3((unsigned)blocks), dim3(256), 0, st, plan->d_nodes,
+                               plan->d_children, L, bb);
+        else
+            hipLaunchKernelGGL(k_chunk_level<false>, dim3((unsigned)blocks), dim3(256), 0, st, plan->d_nodes,
+                               plan->d_children, L, bb);
+        if (timer_end) timer_end(tctx, kid);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (p.top_h <= p.height) {
+        if (p.height > TOP_MAX_H) return hipErrorInvalidValue;
+        TopLevels tl{};
+        tl.h0 = p.top_h;
+        tl.h1 = p.height;
+        for (int h = 1; h <= p.height; h++) {
+            tl.hb[h - 1] = p.lvl_hfull_begin[h - 1];
+            tl.he[h - 1] = p.lvl_hfull_end[h - 1];
+            tl.gb[h - 1] = p.lvl_gen_begin[h - 1];
+            tl.ge[h - 1] = p.lvl_gen_end[h - 1];
+        }
+        if (timer_begin) timer_begin(tctx, GSV_K_CHUNK_LEVEL);
+        hipLaunchKernelGGL(k_chunk_top, dim3(nb), dim3(TOP_BLOCK), 0, st, plan->d_nodes, plan->d_children, tl, bb);
+        if (timer_end) timer_end(tctx, GSV_K_CHUNK_LEVEL);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies, const uint64_t* d_body_off,
@@ -600,27 +800,7 @@ hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies,
     bb.leafrefs = nullptr;
     bb.leaf_base = nullptr;
     bb.generic = 0;
-    for (int h = 1; h <= p.height; h++) {
-        int b0 = p.lvl_bottom_begin[h - 1], b1 = p.lvl_bottom_end[h - 1];
-        if (b1 > b0) {
-            uint64_t total = (uint64_t)(b1 - b0) * nbodies;
-            if (timer_begin) timer_begin(tctx, GSV_K_CHUNK_LEAF);
-            hipLaunchKernelGGL(k_chunk_bottom, dim3((unsigned)((total + BOT_BLOCK - 1) / BOT_BLOCK)),
-                               dim3(BOT_BLOCK), 0, st, plan->d_nodes, b0, b1 - b0, bb);
-            if (timer_end) timer_end(tctx, GSV_K_CHUNK_LEAF);
-        }
-        int g0 = p.lvl_gen_begin[h - 1], g1 = p.lvl_gen_end[h - 1];
-        if (g1 > g0) {
-            uint64_t total = (uint64_t)(g1 - g0) * nbodies;
-            if (timer_begin) timer_begin(tctx, GSV_K_CHUNK_LEVEL);
-            hipLaunchKernelGGL(k_chunk_level, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
-                               plan->d_nodes, plan->d_children, g0, g1 - g0, bb);
-            if (timer_end) timer_end(tctx, GSV_K_CHUNK_LEVEL);
-        }
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    return launch_levels(plan, bb, st, timer_begin, timer_end, tctx);
 }
 
 // ================================================================ generic DeriveSha (any DerivableList)
@@ -660,7 +840,7 @@ __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__
     bool vbyte = (L == 1 && v[0] < 0x80);
     uint32_t venc = vbyte ? 1u : prefix_len(L) + L;
     uint8_t* m = lmsg + lmsg_off[item];
-    Writer w{m, 0, false};
+    Writer w{m, 0};
     put_prefix(w, 0xc0, kenc + venc);
     w.str(ck, cl);
     if (vbyte) {
@@ -674,16 +854,8 @@ __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__
     if (N == 1 || len >= 32) {
         uint32_t h[8];
         keccak_buf(h, m, len);
-        if (N == 1) {
-            uint8_t* o = roots + (size_t)b * 32;
-#pragma unroll
-            for (int q = 0; q < 8; q++)
-#pragma unroll
-                for (int y = 0; y < 4; y++) o[4 * q + y] = (uint8_t)(h[q] >> (8 * y));
-        } else {
-            s[0] = 33;
-            put_hashref(s + 8, h);
-        }
+        if (N == 1) store_hash32(roots + (size_t)b * 32, h);
+        else store_hashref_slot(s, h);
     } else {
         s[0] = (uint8_t)len;
         for (uint32_t k = 0; k < len; k++) s[8 + k] = m[k];
@@ -720,18 +892,7 @@ hipError_t launch_derive_sha_plan(const TriePlan* plan, uint32_t nlists, const u
     bb.leafrefs = d_leafrefs;
     bb.leaf_base = d_leaf_base;
     bb.generic = 1;
-    for (int h = 1; h <= p.height; h++) {
-        int g0 = p.lvl_gen_begin[h - 1], g1 = p.lvl_gen_end[h - 1];
-        if (g1 <= g0) continue;
-        uint64_t tot = (uint64_t)(g1 - g0) * nlists;
-        if (timer_begin) timer_begin(tctx, GSV_K_CHUNK_LEVEL);
-        hipLaunchKernelGGL(k_chunk_level, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, plan->d_nodes,
-                           plan->d_children, g0, g1 - g0, bb);
-        if (timer_end) timer_end(tctx, GSV_K_CHUNK_LEVEL);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    return launch_levels(plan, bb, st, timer_begin, timer_end, tctx);
 }
 
 // ================================================================ Proof of Custody body expansion
