@@ -148,6 +148,7 @@ def main():
     ap.add_argument("--no-chunk-leg", action="store_true")
     ap.add_argument("--no-pairing-leg", action="store_true")
     ap.add_argument("--no-notary-leg", action="store_true")
+    ap.add_argument("--no-extra-legs", action="store_true", help="skip the §8f row 2-3 legs (tx roots, POC, headers)")
     args = ap.parse_args()
 
     import torch
@@ -288,6 +289,83 @@ def main():
             "scaling": "strong",
         }
 
+    # ---------------------------------------------------------------- §8f rows 2-3 (not BASELINE configs)
+    extras = None
+    if not args.no_extra_legs:
+        extras = {}
+        # tx roots (core/block_validator.go:70 DeriveSha(block.Transactions())): 2,000 blocks x 200
+        # RLP txs of 100-160 bytes (random bytes: the trie only sees the item strings)
+        rng = np.random.default_rng(11 + rank)
+        nblk, ntx = 2000, 200
+        lens = rng.integers(100, 161, nblk * ntx).astype(np.uint64)
+        voff = np.zeros(nblk * ntx + 1, np.uint64)
+        np.cumsum(lens, out=voff[1:])
+        vals = torch.from_numpy(rng.integers(0, 256, int(voff[-1]), dtype=np.uint8)).to(dev)
+        list_off = np.arange(nblk + 1, dtype=np.uint64) * ntx
+        troots = torch.empty((nblk, 32), dtype=torch.uint8, device=dev)
+        ctx.derive_sha_batch_dev(vals, voff, list_off, troots, stream=stream)
+        stream.synchronize()
+        tsteps = 3
+        barrier(ws)
+        t5 = time.perf_counter()
+        for _ in range(tsteps):
+            ctx.derive_sha_batch_dev(vals, voff, list_off, troots, stream=stream)
+        stream.synchronize()
+        barrier(ws)
+        tdt = max_over_ranks(time.perf_counter() - t5, ws)
+        extras["tx_root"] = {"blocks_per_s": round(ws * nblk * tsteps / tdt, 1),
+                             "txs_per_s": round(ws * nblk * ntx * tsteps / tdt, 1),
+                             "MBps_of_tx_rlp": round(ws * float(voff[-1]) * tsteps / tdt / 1e6, 1),
+                             "blocks": nblk, "txs_per_block": ntx, "ms_per_step": round(tdt / tsteps * 1e3, 3)}
+        del vals
+        # Proof of Custody (sharding/collation.go:124-136): 100 x 1 MiB bodies, 20-byte salt
+        # (sharding/collation_test.go:318) -> 21 MiB salted chunk tries
+        prng = np.random.default_rng(13 + rank)
+        pbodies = torch.from_numpy(prng.integers(0, 256, N_SHARDS * BODY, dtype=np.uint8)).to(dev)
+        p_off2 = np.arange(N_SHARDS + 1, dtype=np.uint64) * BODY
+        salt = bytes(range(1, 21))
+        pocs = torch.empty((N_SHARDS, 32), dtype=torch.uint8, device=dev)
+        ctx.collation_poc_batch_dev(pbodies, p_off2, salt, pocs, stream=stream)
+        stream.synchronize()
+        qsteps = 2
+        barrier(ws)
+        t6 = time.perf_counter()
+        for _ in range(qsteps):
+            ctx.collation_poc_batch_dev(pbodies, p_off2, salt, pocs, stream=stream)
+        stream.synchronize()
+        barrier(ws)
+        qdt = max_over_ranks(time.perf_counter() - t6, ws)
+        extras["proof_of_custody"] = {"bodies_per_s": round(ws * N_SHARDS * qsteps / qdt, 2),
+                                      "body_GBps": round(ws * N_SHARDS * BODY * qsteps / qdt / 1e9, 3),
+                                      "salted_GBps": round(ws * N_SHARDS * BODY * 21 * qsteps / qdt / 1e9, 3),
+                                      "salt_bytes": 20, "ms_per_step": round(qdt / qsteps * 1e3, 3)}
+        del pbodies
+        # collation header hash + proposer signature: 2^20 headers with random fields and valid ECDSA
+        # signatures over other messages -> every status GSV_ST_PROPOSER_MISMATCH (same work as a match)
+        nh = 1 << 20
+        hsid = torch.randint(0, 256, (nh, 32), dtype=torch.uint8, device=dev)
+        hroot = torch.randint(0, 256, (nh, 32), dtype=torch.uint8, device=dev)
+        hper = torch.randint(0, 256, (nh, 32), dtype=torch.uint8, device=dev)
+        hprop = torch.randint(0, 256, (nh, 20), dtype=torch.uint8, device=dev)
+        hst = torch.empty((nh,), dtype=torch.uint8, device=dev)
+        hhash = torch.empty((nh, 32), dtype=torch.uint8, device=dev)
+        hsigner = torch.empty((nh, 20), dtype=torch.uint8, device=dev)
+        ctx.collation_header_verify_batch_dev(hsid, hroot, hper, hprop, sig, hst, None, hhash, hsigner,
+                                              stream=stream)
+        stream.synchronize()
+        assert bool((hst == _lib.ST_PROPOSER_MISMATCH).all()), "header signatures failed to recover"
+        hsteps = 3
+        barrier(ws)
+        t7 = time.perf_counter()
+        for _ in range(hsteps):
+            ctx.collation_header_verify_batch_dev(hsid, hroot, hper, hprop, sig, hst, None, hhash, hsigner,
+                                                  stream=stream)
+        stream.synchronize()
+        barrier(ws)
+        hdt = max_over_ranks(time.perf_counter() - t7, ws)
+        extras["collation_headers"] = {"headers_per_s": round(ws * nh * hsteps / hdt, 1), "headers": nh,
+                                       "ms_per_step": round(hdt / hsteps * 1e3, 3)}
+
     # ---------------------------------------------------------------- pairing leg (configs[4])
     pairing = None
     if not args.no_pairing_leg:
@@ -404,6 +482,8 @@ def main():
             line["bn256_pairing"] = pairing
         if notary is not None:
             line["notary"] = notary
+        if extras is not None:
+            line["collation_extras"] = extras
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist

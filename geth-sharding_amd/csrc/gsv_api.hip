@@ -1043,6 +1043,24 @@ int gsv_collation_poc_batch(gsv_ctx* c, const uint8_t* bodies, const uint64_t* o
 }
 
 // ------------------------------------------------------------------ collation header + proposer signature
+int gsv_collation_header_verify_batch_dev(gsv_ctx* c, const uint8_t* d_sid, const uint8_t* d_root,
+                                          const uint8_t* d_per, const uint8_t* d_prop, const uint8_t* d_sig,
+                                          const uint8_t* d_nil, size_t n, uint8_t* d_hash, uint8_t* d_signer,
+                                          uint8_t* d_st, void* stream) {
+    if (!c || (n && (!d_sid || !d_root || !d_per || !d_prop || !d_sig || !d_st))) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    if (n > (1u << 30)) return GSV_E_TOO_LARGE;
+    std::lock_guard<std::mutex> g(c->wmu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int rc = work_reserve(c, al(gsv::header_scratch_bytes((uint32_t)n)));
+    if (rc) return rc;
+    KTimer t(c, GSV_K_HEADER, st);
+    HIPCHK(gsv::launch_header_verify(d_sid, d_root, d_per, d_prop, d_sig, d_nil, (uint32_t)n, c->gtab, c->work,
+                                     d_hash, d_signer, d_st, st));
+    return GSV_SUCCESS;
+}
+
 int gsv_collation_header_verify_batch(gsv_ctx* c, const uint8_t* shard_id32, const uint8_t* chunk_root32,
                                       const uint8_t* period32, const uint8_t* proposer20, const uint8_t* sig65,
                                       const uint8_t* nil_flags, size_t n, uint8_t* hash32_out,

@@ -374,6 +374,16 @@ def _collation_header_verify_batch(self, shard_id32, chunk_root32, period32, pro
     return h, signer, st
 
 
+def _collation_header_verify_batch_dev(self, sid_t, root_t, per_t, prop_t, sig_t, st_t, nil_t=None, hash_t=None,
+                                       signer_t=None, stream=None):
+    n = sid_t.shape[0]
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_collation_header_verify_batch_dev(self._h, _tptr(sid_t), _tptr(root_t), _tptr(per_t),
+                                                            _tptr(prop_t), _tptr(sig_t), _tptr(nil_t), n,
+                                                            _tptr(hash_t), _tptr(signer_t), _tptr(st_t), sp))
+
+
+Context.collation_header_verify_batch_dev = _collation_header_verify_batch_dev
 Context.derive_sha_batch = _derive_sha_batch
 Context.derive_sha_batch_dev = _derive_sha_batch_dev
 Context.collation_poc_batch = _collation_poc_batch

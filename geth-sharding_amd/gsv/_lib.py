@@ -87,6 +87,8 @@ SIGNATURES = [
     ("gsv_collation_poc_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp]),
     ("gsv_collation_poc_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp]),
     ("gsv_collation_header_verify_batch", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    ("gsv_collation_header_verify_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp,
+                                                             _vp]),
 ]
 
 _lib = None

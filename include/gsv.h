@@ -241,6 +241,13 @@ int gsv_collation_header_verify_batch(gsv_ctx *ctx, const uint8_t *shard_id32, c
                                       const uint8_t *period32, const uint8_t *proposer20, const uint8_t *sig65,
                                       const uint8_t *nil_flags, size_t n, uint8_t *hash32_out,
                                       uint8_t *signer20_out, uint8_t *status);
+/* Device-resident form: every array in HBM (d_nil_flags / d_hash32_out / d_signer20_out may be NULL);
+ * enqueues on `stream` (NULL = the context stream) and returns. */
+int gsv_collation_header_verify_batch_dev(gsv_ctx *ctx, const uint8_t *d_shard_id32, const uint8_t *d_chunk_root32,
+                                          const uint8_t *d_period32, const uint8_t *d_proposer20,
+                                          const uint8_t *d_sig65, const uint8_t *d_nil_flags, size_t n,
+                                          uint8_t *d_hash32_out, uint8_t *d_signer20_out, uint8_t *d_status,
+                                          void *stream);
 
 #ifdef __cplusplus
 }
