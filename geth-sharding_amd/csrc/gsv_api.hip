@@ -42,6 +42,13 @@ struct gsv_ctx {
     size_t nwork_cap = 0;
     uint8_t* pwork = nullptr;         // Proof-of-Custody salted bodies (outlive `work` regrowth)
     size_t pwork_cap = 0;
+    // ordering of `work` users on different streams: the last user's stream + an event after its work
+    hipStream_t work_st = nullptr;
+    hipEvent_t work_ev = nullptr;
+    // chunk-root body offsets cached on the device (re-uploaded only when they change)
+    uint64_t* coff = nullptr;
+    size_t coff_cap = 0;
+    std::vector<uint64_t> coff_key;
 };
 
 namespace {
@@ -138,6 +145,17 @@ int work_reserve(gsv_ctx* c, size_t bytes) {
     return GSV_SUCCESS;
 }
 
+// `work` is shared by the *_dev paths of one context: a call on a stream other than the previous
+// user's waits (on the GPU) for that user's last enqueued work before touching it.
+void work_begin(gsv_ctx* c, hipStream_t st) {
+    if (c->work_st && c->work_st != st && c->work_ev) hipStreamWaitEvent(st, c->work_ev, 0);
+}
+void work_end(gsv_ctx* c, hipStream_t st) {
+    if (!c->work_ev) hipEventCreateWithFlags(&c->work_ev, hipEventDisableTiming);
+    if (c->work_ev) hipEventRecord(c->work_ev, st);
+    c->work_st = st;
+}
+
 int arena_reserve(gsv_ctx* c, size_t bytes) {
     if (bytes <= c->arena_cap) return GSV_SUCCESS;
     size_t cap = c->arena_cap ? c->arena_cap : (size_t)64 << 20;
@@ -232,6 +250,8 @@ void gsv_ctx_destroy(gsv_ctx* c) {
     if (c->work) hipFree(c->work);
     if (c->nwork) hipFree(c->nwork);
     if (c->pwork) hipFree(c->pwork);
+    if (c->coff) hipFree(c->coff);
+    if (c->work_ev) hipEventDestroy(c->work_ev);
     if (c->gtab) hipFree(c->gtab);
     hipStreamDestroy(c->stream);
     delete c;
@@ -420,19 +440,38 @@ static int chunk_root_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64
         groups[end[i] - start[i]].push_back((uint32_t)i);
     }
     size_t need = 0;
+    std::vector<uint64_t> key;  // all groups' body offsets, in group order
+    key.reserve(n);
     for (auto& g : groups) {
         if (g.first == 0) continue;
         gsv::TriePlan* pl = c->plans.get((uint32_t)g.first);
         if (!pl) return GSV_E_NOMEM;
-        need += al(g.second.size() * 8) + al(g.second.size() * 32) +
-                al(gsv::chunk_root_scratch_bytes(pl, (uint32_t)g.second.size()));
+        need += al(g.second.size() * 32) + al(gsv::chunk_root_scratch_bytes(pl, (uint32_t)g.second.size()));
+        for (uint32_t i : g.second) key.push_back(start[i]);
     }
+    work_begin(c, st);
     int rc = work_reserve(c, need + 4096);
     if (rc) return rc;
+    // device copy of the offsets: uploaded only when they differ from the previous call's
+    if (key != c->coff_key) {
+        if (key.size() * 8 > c->coff_cap) {
+            if (c->coff) {
+                hipDeviceSynchronize();
+                hipFree(c->coff);
+                c->coff = nullptr;
+                c->coff_cap = 0;
+            }
+            size_t cap = (key.size() * 8 + 4095) & ~(size_t)4095;
+            if (hipMalloc(&c->coff, cap) != hipSuccess) return GSV_E_NOMEM;
+            c->coff_cap = cap;
+        }
+        if (!key.empty())  // pageable source: staged before return, so `key` may go out of scope
+            HIPCHK(hipMemcpyAsync(c->coff, key.data(), key.size() * 8, hipMemcpyHostToDevice, st));
+        c->coff_key = std::move(key);
+    }
     Carve cv(c->work);
     c->cur_stream = st;
-    std::vector<std::vector<uint64_t>> host_offs;
-    host_offs.reserve(groups.size());
+    size_t koff = 0;
     for (auto& g : groups) {
         const auto& idx = g.second;
         if (g.first == 0) {  // empty trie -> emptyRoot (trie/trie.go:472-474)
@@ -441,15 +480,13 @@ static int chunk_root_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64
             continue;
         }
         gsv::TriePlan* pl = c->plans.get((uint32_t)g.first);
-        uint64_t* d_off = cv.take<uint64_t>(idx.size() * 8);
-        uint8_t* d_gr = cv.take<uint8_t>(idx.size() * 32);
+        bool direct = idx.size() == n;  // one group holding bodies 0..n-1 in order: roots in place
+        uint8_t* d_gr = direct ? d_roots : cv.take<uint8_t>(idx.size() * 32);
         uint8_t* d_scr = cv.take<uint8_t>(gsv::chunk_root_scratch_bytes(pl, (uint32_t)idx.size()));
-        host_offs.emplace_back(idx.size());
-        auto& ho = host_offs.back();
-        for (size_t k = 0; k < idx.size(); k++) ho[k] = start[idx[k]];
-        HIPCHK(hipMemcpyAsync(d_off, ho.data(), ho.size() * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(gsv::launch_chunk_root_plan(pl, d_bodies, d_off, (uint32_t)idx.size(), d_scr, d_gr, st,
+        HIPCHK(gsv::launch_chunk_root_plan(pl, d_bodies, c->coff + koff, (uint32_t)idx.size(), d_scr, d_gr, st,
                                            hook_begin, hook_end, c));
+        koff += idx.size();
+        if (direct) continue;
         // scatter group roots to their positions (contiguous runs copied together)
         size_t k = 0;
         while (k < idx.size()) {
@@ -460,7 +497,7 @@ static int chunk_root_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64
             k = e2;
         }
     }
-    HIPCHK(hipStreamSynchronize(st));  // host offset staging must outlive the async copies
+    work_end(c, st);
     return GSV_SUCCESS;
 }
 
@@ -633,6 +670,7 @@ static int bn_run(gsv_ctx* c, const uint8_t* d_in, const BnTables& t, size_t n, 
                   hipStream_t st) {
     size_t np = t.pair_src.size();
     size_t need = al(np * 8 + 8) + al((n + 1) * 4) + al(np + 1) + al(np * 48 * 4 + 4) + al(np * 96 * 4 + 4);
+    work_begin(c, st);
     int rc = work_reserve(c, need + 4096);
     if (rc) return rc;
     Carve cv(c->work);
@@ -719,6 +757,7 @@ static int notary_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* 
     if (cidlen > 64) return GSV_E_INVALID_ARG;
     for (size_t i = 0; i < n; i++)
         if (end[i] < start[i] || end[i] - start[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+    work_begin(c, st);  // nwork / work of a previous call may still be in use on another stream
     // chain-id buffers: 64-byte big-endian value and the sighash suffix rlp(chainId) || 0x80 0x80
     uint8_t host[256] = {0};
     memcpy(host + 64 - cidlen, cid, cidlen);
@@ -872,6 +911,7 @@ static int derive_sha_dev_impl(gsv_ctx* c, const uint8_t* d_vals, const uint64_t
         need += al(g.second.size() * 8) + al(g.second.size() * 32) +
                 al(gsv::derive_sha_scratch_bytes(pl, (uint32_t)g.second.size()));
     }
+    work_begin(c, st);
     int rc = work_reserve(c, need + 4096);
     if (rc) return rc;
     Carve cv(c->work);
@@ -958,6 +998,7 @@ static const uint64_t MAX_POC = 1ull << 26;
 
 static int poc_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* start, const uint64_t* end, size_t n,
                         const uint8_t* salt, size_t slen, uint8_t* d_poc, hipStream_t st) {
+    work_begin(c, st);  // pwork of a previous call may still be read on another stream
     std::vector<uint64_t> io(2 * n), oo(n), os(n), oe(n);
     uint64_t pos = 0, mx = 0;
     for (size_t i = 0; i < n; i++) {
@@ -995,8 +1036,7 @@ static int poc_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* sta
     HIPCHK(hipMemcpyAsync(d_oo, oo.data(), n * 8, hipMemcpyHostToDevice, st));
     if (slen) HIPCHK(hipMemcpyAsync(d_salt, salt, slen, hipMemcpyHostToDevice, st));
     HIPCHK(gsv::launch_poc_expand(d_bodies, d_io, d_oo, (uint32_t)n, mx, d_salt, (uint32_t)slen, d_out, st));
-    int rc = chunk_root_dev_impl(c, d_out, os.data(), oe.data(), n, d_poc, st, MAX_POC);
-    return rc;  // chunk_root_dev_impl synchronizes the stream before returning
+    return chunk_root_dev_impl(c, d_out, os.data(), oe.data(), n, d_poc, st, MAX_POC);
 }
 
 int gsv_collation_poc_batch_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n,
@@ -1053,11 +1093,15 @@ int gsv_collation_header_verify_batch_dev(gsv_ctx* c, const uint8_t* d_sid, cons
     std::lock_guard<std::mutex> g(c->wmu);
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    work_begin(c, st);
     int rc = work_reserve(c, al(gsv::header_scratch_bytes((uint32_t)n)));
     if (rc) return rc;
-    KTimer t(c, GSV_K_HEADER, st);
-    HIPCHK(gsv::launch_header_verify(d_sid, d_root, d_per, d_prop, d_sig, d_nil, (uint32_t)n, c->gtab, c->work,
-                                     d_hash, d_signer, d_st, st));
+    {
+        KTimer t(c, GSV_K_HEADER, st);
+        HIPCHK(gsv::launch_header_verify(d_sid, d_root, d_per, d_prop, d_sig, d_nil, (uint32_t)n, c->gtab, c->work,
+                                         d_hash, d_signer, d_st, st));
+    }
+    work_end(c, st);
     return GSV_SUCCESS;
 }
 
