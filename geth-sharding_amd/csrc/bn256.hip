@@ -1,14 +1,14 @@
 // Batched BN254 PairingCheck on gfx950 (bn256.PairingCheck as driven by the bn256Pairing
 // precompile, core/vm/contracts.go:333-360; crypto/bn256/cloudflare/bn256.go:313-327).
 //
-// One lane per pair for decode + G2 subgroup check + Miller loop, one lane per check for the
-// product of Miller values + final exponentiation.  Three launches:
+// One lane per pair for decode + G2 subgroup check, one lane per check for the multi-Miller loop
+// and the final exponentiation.  Three launches:
 //   k_bn_prepare  decode the 192-byte pair (bn256.go:120-164 G1.Unmarshal, :256-306 G2.Unmarshal):
 //                 coordinates < p, Montgomery encode, infinity detection, y^2 = x^3 + 3 on G1,
-//                 on-twist + Order*Q == infinity on G2 (twist.go:47-63)  -> pair status + points
-//   k_bn_miller   optimal-ate Miller loop (optate.go:122-210)             -> F_p^12 per pair
-//   k_bn_final    acc = prod of the check's Miller values (skipping infinity pairs),
-//                 finalExponentiation (optate.go:212-261), IsOne          -> verdict per check
+//                 on-twist + subgroup membership on G2 (twist.go:47-63)  -> pair status + points
+//   k_bn_miller   optimal-ate Miller loop (optate.go:122-210) over all of a check's pairs with one
+//                 shared accumulator (the product of the per-pair values) -> F_p^12 per check
+//   k_bn_final    finalExponentiation (optate.go:212-261), IsOne          -> verdict per check
 // HBM layout is structure-of-arrays, word-major ([word][pair]), so each lane's word loads and
 // stores coalesce across the wave.
 #include "bn254_dev.cuh"
@@ -536,48 +536,145 @@ __global__ __launch_bounds__(64) void k_bn_prepare(const uint8_t* __restrict__ i
     soa_store(pts, npairs, i, 5, Q.y.y);
 }
 
-__global__ __launch_bounds__(64) void k_bn_miller(const uint8_t* __restrict__ pstat,
-                                                  const uint32_t* __restrict__ pts, uint32_t npairs,
-                                                  uint32_t* __restrict__ fv /* [96 words][npairs] */) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npairs) return;
-    if (pstat[i] != PS_OK) return;
-    g1a P;
-    g2a Q;
-    soa_load(P.x, pts, npairs, i, 0);
-    soa_load(P.y, pts, npairs, i, 1);
-    soa_load(Q.x.x, pts, npairs, i, 2);
-    soa_load(Q.x.y, pts, npairs, i, 3);
-    soa_load(Q.y.x, pts, npairs, i, 4);
-    soa_load(Q.y.y, pts, npairs, i, 5);
-    fp12 f;
-    miller(f, Q, P);
-    fp12_store(fv, npairs, i, f);
+// ---- per-check multi-Miller loop.  The product of a check's Miller values equals one loop that
+// squares the shared accumulator once per step and multiplies in every pair's lines
+// (prod f_i^2 l_i = (prod f_i)^2 prod l_i, exact in F_p^12), so a check of k pairs spends one
+// F_p^12 squaring per step instead of k; the verdict is the reference's bit for bit.  One lane per
+// check; pair j of a check lives at slot-major index pidx[first + j] (the j-th pairs of all checks
+// contiguous), so the per-pair twist point R and the decoded points load/store coalesced.
+enum : uint8_t { CS_OK = 0, CS_BAD = 1, CS_ONE = 2 };  // CS_ONE: no finite pair -> product is 1
+
+GSV_DI void g2j_load(g2j& r, const uint32_t* __restrict__ base, uint32_t n, uint32_t i) {
+    soa_load(r.x.x, base, n, i, 0);
+    soa_load(r.x.y, base, n, i, 1);
+    soa_load(r.y.x, base, n, i, 2);
+    soa_load(r.y.y, base, n, i, 3);
+    soa_load(r.z.x, base, n, i, 4);
+    soa_load(r.z.y, base, n, i, 5);
+    soa_load(r.t.x, base, n, i, 6);
+    soa_load(r.t.y, base, n, i, 7);
+}
+GSV_DI void g2j_store(uint32_t* __restrict__ base, uint32_t n, uint32_t i, const g2j& r) {
+    soa_store(base, n, i, 0, r.x.x);
+    soa_store(base, n, i, 1, r.x.y);
+    soa_store(base, n, i, 2, r.y.x);
+    soa_store(base, n, i, 3, r.y.y);
+    soa_store(base, n, i, 4, r.z.x);
+    soa_store(base, n, i, 5, r.z.y);
+    soa_store(base, n, i, 6, r.t.x);
+    soa_store(base, n, i, 7, r.t.y);
+}
+GSV_DI void pts_load(g1a& P, g2a& Q, const uint32_t* __restrict__ pts, uint32_t n, uint32_t j) {
+    soa_load(P.x, pts, n, j, 0);
+    soa_load(P.y, pts, n, j, 1);
+    soa_load(Q.x.x, pts, n, j, 2);
+    soa_load(Q.x.y, pts, n, j, 3);
+    soa_load(Q.y.x, pts, n, j, 4);
+    soa_load(Q.y.y, pts, n, j, 5);
 }
 
-__global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ check_first,
-                                                 uint32_t nchecks, const uint8_t* __restrict__ pstat,
-                                                 const uint32_t* __restrict__ fv, uint32_t npairs,
-                                                 uint8_t* __restrict__ verdict) {
+__global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ check_first, uint32_t nchecks,
+                                                  const uint32_t* __restrict__ pidx, const uint8_t* __restrict__ pstat,
+                                                  const uint32_t* __restrict__ pts, uint32_t npairs,
+                                                  uint32_t* __restrict__ rs /* [64 words][npairs] */,
+                                                  uint8_t* __restrict__ cstat,
+                                                  uint32_t* __restrict__ fv /* [96 words][nchecks] */) {
     uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchecks) return;
     uint32_t b = check_first[c], e = check_first[c + 1];
     bool bad = false, any = false;
-    fp12 acc;
-    fp12_one(acc);
-    for (uint32_t p = b; p < e; p++) {
-        uint8_t st = pstat[p];
+    for (uint32_t q = b; q < e; q++) {
+        uint32_t j = pidx[q];
+        uint8_t st = pstat[j];
         bad = bad || st == PS_BAD;
         if (st != PS_OK) continue;
-        fp12 f;
-        fp12_load(f, fv, npairs, p);
-        if (!any) acc = f;  // 1 * f == f exactly (canonical residues)
-        else fp12_mul(acc, acc, f);
         any = true;
+        g1a P;
+        g2a Q;
+        pts_load(P, Q, pts, npairs, j);
+        g2j r;
+        r.x = Q.x;
+        r.y = Q.y;
+        fp2_one(r.z);
+        fp2_one(r.t);
+        g2j_store(rs, npairs, j, r);
     }
+    cstat[c] = bad ? CS_BAD : any ? CS_OK : CS_ONE;
+    if (bad || !any) return;
+    fp12 f;
+    fp12_one(f);
+    fp2 la, lb, lc;
+#pragma unroll 1
+    for (int i = 64; i > 0; i--) {
+        if (i != 64) fp12_sqr(f, f);
+        uint64_t bit = 1ull << (i - 1);
+        bool add = ((NAF_POS | NAF_NEG) & bit) != 0;
+        for (uint32_t q = b; q < e; q++) {
+            uint32_t j = pidx[q];
+            if (pstat[j] != PS_OK) continue;
+            g1a P;
+            g2a Q;
+            pts_load(P, Q, pts, npairs, j);
+            g2j r;
+            g2j_load(r, rs, npairs, j);
+            line_double(la, lb, lc, r, P);
+            mul_line(&f, &la, &lb, &lc);
+            if (add) {
+                fp2 r2;
+                fp2_sqr(r2, Q.y);
+                if (NAF_NEG & bit) fp2_neg(Q.y, Q.y);
+                line_add(la, lb, lc, r, Q, P, r2);
+                mul_line(&f, &la, &lb, &lc);
+            }
+            g2j_store(rs, npairs, j, r);
+        }
+    }
+    // Q1 = pi(Q), -Q2 = -pi^2(Q) (optate.go:168-209), per pair
+    for (uint32_t q = b; q < e; q++) {
+        uint32_t j = pidx[q];
+        if (pstat[j] != PS_OK) continue;
+        g1a P;
+        g2a A;
+        pts_load(P, A, pts, npairs, j);
+        g2j r;
+        g2j_load(r, rs, npairs, j);
+        g2a q1, mq2;
+        fp2 k, r2;
+        fp2_conj(q1.x, A.x);
+        fp2_const(k, XI_P1_3_X, XI_P1_3_Y);
+        fp2_mul(q1.x, q1.x, k);
+        fp2_conj(q1.y, A.y);
+        fp2_const(k, XI_P1_2_X, XI_P1_2_Y);
+        fp2_mul(q1.y, q1.y, k);
+        fp kk;
+        fp_const(kk, XI_PSQ1_3);
+        fp2_mul_fp(mq2.x, A.x, kk);
+        mq2.y = A.y;
+        fp2_sqr(r2, q1.y);
+        line_add(la, lb, lc, r, q1, P, r2);
+        mul_line(&f, &la, &lb, &lc);
+        fp2_sqr(r2, mq2.y);
+        line_add(la, lb, lc, r, mq2, P, r2);
+        mul_line(&f, &la, &lb, &lc);
+    }
+    fp12_store(fv, nchecks, c, f);
+}
+
+__global__ __launch_bounds__(64) void k_bn_final(uint32_t nchecks, const uint8_t* __restrict__ cstat,
+                                                 const uint32_t* __restrict__ fv, uint8_t* __restrict__ verdict) {
+    uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchecks) return;
+    uint8_t cs = cstat[c];
+    if (cs == CS_BAD) {
+        verdict[c] = GSV_PAIRING_BAD_INPUT;
+        return;
+    }
+    fp12 acc;
+    if (cs == CS_ONE) fp12_one(acc);  // finalExponentiation(1) == 1 (all pairs at infinity / no pairs)
+    else fp12_load(acc, fv, nchecks, c);
     fp12 r;
     final_exp(&r, &acc);
-    verdict[c] = bad ? GSV_PAIRING_BAD_INPUT : fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
+    verdict[c] = fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
 }
 
 
@@ -801,9 +898,10 @@ hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, u
 }
 
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
-                                const uint32_t* d_check_first, uint32_t nchecks, uint8_t* d_pstat,
-                                uint32_t* d_pts, uint32_t* d_fv, uint8_t* d_verdict, hipStream_t st,
-                                void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx) {
+                                const uint32_t* d_check_first, const uint32_t* d_pidx, uint32_t nchecks,
+                                uint8_t* d_pstat, uint32_t* d_pts, uint32_t* d_rs, uint8_t* d_cstat, uint32_t* d_fv,
+                                uint8_t* d_verdict, hipStream_t st, void (*timer_begin)(void*, int),
+                                void (*timer_end)(void*, int), void* tctx) {
     if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
         hipLaunchKernelGGL(bn::k_bn_prepare, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
@@ -811,16 +909,17 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
-        hipLaunchKernelGGL(bn::k_bn_miller, dim3((npairs + 63) / 64), dim3(64), 0, st, d_pstat, d_pts, npairs, d_fv);
-        if (timer_end) timer_end(tctx, GSV_K_PAIRING);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
     }
     if (nchecks) {
+        if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
+        hipLaunchKernelGGL(bn::k_bn_miller, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_first, nchecks,
+                           d_pidx, d_pstat, d_pts, npairs, d_rs, d_cstat, d_fv);
+        if (timer_end) timer_end(tctx, GSV_K_PAIRING);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
-        hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_first, nchecks,
-                           d_pstat, d_fv, npairs, d_verdict);
+        hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, nchecks, d_cstat, d_fv,
+                           d_verdict);
         if (timer_end) timer_end(tctx, GSV_K_BN_FINAL);
     }
     return hipGetLastError();

@@ -4,6 +4,7 @@
 // synchronize (graph-capturable).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -639,29 +640,59 @@ int gsv_tx_sender_batch(gsv_ctx* c, const uint8_t* rlp, const uint64_t* off, siz
 // Host tables for a batch: check c = in[off[c] .. off[c+1]); a length that is not a multiple of
 // 192 is errBadPairingInput (core/vm/contracts.go:336-338) and contributes no pairs.
 struct BnTables {
-    std::vector<uint64_t> pair_src;
-    std::vector<uint32_t> check_first;
+    std::vector<uint64_t> pair_src;     // slot-major pair order
+    std::vector<uint32_t> check_first;  // check c's pairs: pidx[check_first[c] .. check_first[c+1])
+    std::vector<uint32_t> pidx;         // check-major position -> slot-major pair index
     std::vector<uint8_t> bad_len;
 };
 static int bn_tables(const uint64_t* off, size_t n, uint64_t base, BnTables& t) {
     t.check_first.resize(n + 1);
     t.bad_len.assign(n, 0);
-    size_t np = 0;
+    size_t np = 0, maxk = 0;
     for (size_t c = 0; c < n; c++) {
         if (off[c + 1] < off[c]) return GSV_E_INVALID_ARG;
         uint64_t len = off[c + 1] - off[c];
         if (len % 192) t.bad_len[c] = 1;
-        else np += len / 192;
+        else {
+            np += len / 192;
+            maxk = std::max<size_t>(maxk, len / 192);
+        }
     }
     if (np > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
-    t.pair_src.resize(np);
-    size_t k = 0;
+    // slot-major order: slot k holds the k-th pair of every check that has more than k pairs
+    std::vector<uint32_t> per_slot(maxk + 1, 0);
     for (size_t c = 0; c < n; c++) {
-        t.check_first[c] = (uint32_t)k;
         if (t.bad_len[c]) continue;
-        for (uint64_t o = off[c]; o < off[c + 1]; o += 192) t.pair_src[k++] = o - base;
+        per_slot[(off[c + 1] - off[c]) / 192]++;  // histogram of pair counts
     }
-    t.check_first[n] = (uint32_t)k;
+    std::vector<uint64_t> slot_base(maxk + 1, 0), fill(maxk + 1, 0);
+    {
+        uint64_t more = 0;  // checks with > k pairs, from the top
+        std::vector<uint64_t> gt(maxk + 1, 0);
+        for (size_t k = maxk + 1; k-- > 0;) {
+            gt[k] = more;
+            more += per_slot[k];
+        }
+        uint64_t acc = 0;
+        for (size_t k = 0; k < maxk; k++) {
+            slot_base[k] = acc;
+            acc += gt[k];
+        }
+    }
+    t.pair_src.resize(np);
+    t.pidx.resize(np);
+    size_t q = 0;
+    for (size_t c = 0; c < n; c++) {
+        t.check_first[c] = (uint32_t)q;
+        if (t.bad_len[c]) continue;
+        size_t k = 0;
+        for (uint64_t o = off[c]; o < off[c + 1]; o += 192, k++) {
+            uint64_t j = slot_base[k] + fill[k]++;
+            t.pair_src[j] = o - base;
+            t.pidx[q++] = (uint32_t)j;
+        }
+    }
+    t.check_first[n] = (uint32_t)q;
     return GSV_SUCCESS;
 }
 
@@ -669,21 +700,26 @@ static int bn_tables(const uint64_t* off, size_t n, uint64_t base, BnTables& t) 
 static int bn_run(gsv_ctx* c, const uint8_t* d_in, const BnTables& t, size_t n, uint8_t* d_verdict,
                   hipStream_t st) {
     size_t np = t.pair_src.size();
-    size_t need = al(np * 8 + 8) + al((n + 1) * 4) + al(np + 1) + al(np * 48 * 4 + 4) + al(np * 96 * 4 + 4);
+    size_t need = al(np * 8 + 8) + al((n + 1) * 4) + al(np * 4 + 4) + al(np + 1) + al(np * 48 * 4 + 4) +
+                  al(np * 64 * 4 + 4) + al(n + 1) + al(n * 96 * 4 + 4);
     work_begin(c, st);
     int rc = work_reserve(c, need + 4096);
     if (rc) return rc;
     Carve cv(c->work);
     uint64_t* d_src = cv.take<uint64_t>(np * 8 + 8);
     uint32_t* d_first = cv.take<uint32_t>((n + 1) * 4);
+    uint32_t* d_pidx = cv.take<uint32_t>(np * 4 + 4);
     uint8_t* d_pstat = cv.take<uint8_t>(np + 1);
     uint32_t* d_pts = cv.take<uint32_t>(np * 48 * 4 + 4);
-    uint32_t* d_fv = cv.take<uint32_t>(np * 96 * 4 + 4);
+    uint32_t* d_rs = cv.take<uint32_t>(np * 64 * 4 + 4);
+    uint8_t* d_cstat = cv.take<uint8_t>(n + 1);
+    uint32_t* d_fv = cv.take<uint32_t>(n * 96 * 4 + 4);
     if (np) HIPCHK(hipMemcpyAsync(d_src, t.pair_src.data(), np * 8, hipMemcpyHostToDevice, st));
+    if (np) HIPCHK(hipMemcpyAsync(d_pidx, t.pidx.data(), np * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_first, t.check_first.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
     c->cur_stream = st;
-    HIPCHK(gsv::launch_bn256_pairing(d_in, d_src, (uint32_t)np, d_first, (uint32_t)n, d_pstat, d_pts, d_fv,
-                                     d_verdict, st, hook_begin, hook_end, c));
+    HIPCHK(gsv::launch_bn256_pairing(d_in, d_src, (uint32_t)np, d_first, d_pidx, (uint32_t)n, d_pstat, d_pts, d_rs,
+                                     d_cstat, d_fv, d_verdict, st, hook_begin, hook_end, c));
     // errBadPairingInput for ragged lengths overrides the kernel's verdict (those checks had no pairs)
     static const uint8_t bad = GSV_PAIRING_BAD_INPUT;
     for (size_t i = 0; i < n; i++)
