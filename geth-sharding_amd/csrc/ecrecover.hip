@@ -87,28 +87,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     status[i] = (uint8_t)st;
 }
 
-// Fixed-base comb table: entry (w, d) = d * 2^(8w) * G, affine, canonical fe9 limbs
-// (x[9] y[9] + 2 pad words, recover_dev.cuh gtab_load), for d = 1..255 (d = 0 -> G, unused)
-__global__ __launch_bounds__(256) void k_gtable_init(uint4* __restrict__ gtab) {
-    uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= 32 * 256) return;
-    uint32_t w = id >> 8, d = id & 255u;
-    if (d == 0) d = 1;
-    ge9 G;
-    fe9_from_const(G.x, GX);
-    fe9_from_const(G.y, GY);
-    // scalar d << 8w, double-and-add from the top bit
-    gej9 acc;
-    bool inf = true;
-    acc.x = G.x;
-    acc.y = G.y;
-    fe9_set_u32(acc.z, 1);
-    int top = 8 * (int)w + 7;
-    for (int b = top; b >= 0; b--) {
-        if (!inf) gej9_dbl(acc, acc);
-        int bit = (b >= 8 * (int)w) ? (int)((d >> (b - 8 * (int)w)) & 1u) : 0;
-        if (bit) gej9_add_ge(acc, inf, acc, G);
-    }
+// Fixed-base comb table: entry (w, d) = d * 2^(COMB_BITS w) * G, affine, canonical fe9 limbs
+// (x[9] y[9] + 2 pad words, recover_dev.cuh gtab_load).  Built once per context in two launches:
+// k_gtable_base writes each window's base B_w = 2^(COMB_BITS w) G into its unused d = 0 slot, then
+// k_gtable_init computes d * B_w (COMB_BITS-bit double-and-add) for every d >= 1.
+GSV_DI void gtab_store(uint4* e, const gej9& acc) {
     fe9 zi, zi2, x, y;
     fe9_inv(zi, acc.z);
     fe9_sqr(zi2, zi);
@@ -117,12 +100,41 @@ __global__ __launch_bounds__(256) void k_gtable_init(uint4* __restrict__ gtab) {
     fe9_mul(y, acc.y, zi2);
     fe9_normalize_full(x);
     fe9_normalize_full(y);
-    uint4* e = gtab + (size_t)id * GTAB_ENTRY_U4;
     e[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
     e[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
     e[2] = make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]);
     e[3] = make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]);
     e[4] = make_uint4(y.v[7], y.v[8], 0u, 0u);
+}
+
+__global__ __launch_bounds__(64) void k_gtable_base(uint4* __restrict__ gtab) {
+    uint32_t w = threadIdx.x;
+    if (w >= (uint32_t)COMB_WINDOWS) return;
+    gej9 acc;
+    fe9_from_const(acc.x, GX);
+    fe9_from_const(acc.y, GY);
+    fe9_set_u32(acc.z, 1);
+    for (uint32_t k = 0; k < (uint32_t)COMB_BITS * w; k++) gej9_dbl(acc, acc);
+    gtab_store(gtab + ((size_t)w << COMB_BITS) * GTAB_ENTRY_U4, acc);
+}
+
+__global__ __launch_bounds__(256) void k_gtable_init(uint4* __restrict__ gtab) {
+    size_t id = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= GTAB_ENTRIES) return;
+    uint32_t w = (uint32_t)(id >> COMB_BITS), d = (uint32_t)(id & ((1u << COMB_BITS) - 1u));
+    if (d == 0) return;  // holds B_w
+    ge9 B;
+    gtab_load(B, gtab + ((size_t)w << COMB_BITS) * GTAB_ENTRY_U4);
+    gej9 acc;
+    bool inf = true;
+    acc.x = B.x;
+    acc.y = B.y;
+    fe9_set_u32(acc.z, 1);
+    for (int b = COMB_BITS - 1; b >= 0; b--) {
+        if (!inf) gej9_dbl(acc, acc);
+        if ((d >> b) & 1u) gej9_add_ge(acc, inf, acc, B);
+    }
+    gtab_store(gtab + id * GTAB_ENTRY_U4, acc);
 }
 
 // ---------------------------------------------------------------------------- synthetic signer
@@ -152,7 +164,10 @@ __global__ __launch_bounds__(256) void k_synth_sign(uint64_t seed, uint32_t n,
 
 // ---------------------------------------------------------------------------- launchers
 hipError_t launch_gtable_init(uint4* gtab, hipStream_t st) {
-    hipLaunchKernelGGL(k_gtable_init, dim3(32), dim3(256), 0, st, gtab);
+    hipLaunchKernelGGL(k_gtable_base, dim3(1), dim3(64), 0, st, gtab);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gtable_init, dim3((unsigned)((GTAB_ENTRIES + 255) / 256)), dim3(256), 0, st, gtab);
     return hipGetLastError();
 }
 

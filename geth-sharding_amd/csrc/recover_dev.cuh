@@ -186,7 +186,7 @@ GSV_DI void table_select9_x(fe9& out, const fe9 X[4], uint32_t idx) {
     for (int e = 1; e < 4; e++) fe9_cmov(out, X[e], idx == (uint32_t)e);
 }
 
-// comb table entry (w, d) = d * 2^(8w) * G, affine, canonical fe9 limbs: x[9] y[9] + 2 pad words
+// comb table entry (w, d) = d * 2^(COMB_BITS w) * G, affine, canonical fe9 limbs: x[9] y[9] + 2 pad words
 constexpr int GTAB_ENTRY_U4 = GTAB_ENTRY_BYTES / 16;
 GSV_DI void gtab_load(ge9& P, const uint4* e) {
     uint4 a = e[0], b = e[1], c = e[2], d = e[3], f = e[4];
@@ -199,18 +199,24 @@ GSV_DI void gtab_load(ge9& P, const uint4* e) {
     }
 }
 
-// u*G with the byte-window comb table (32 mixed adds, no doublings)
+// window w's digit of the 256-bit scalar u (COMB_BITS divides 32)
+GSV_DI uint32_t comb_digit(const sc& u, uint32_t w) {
+    constexpr uint32_t PER = 32 / COMB_BITS, MASK = (1u << COMB_BITS) - 1u;
+    return (sel_word(u.v, w / PER) >> ((w % PER) * COMB_BITS)) & MASK;
+}
+
+// u*G with the fixed-base comb table (COMB_WINDOWS mixed adds, no doublings)
 GSV_DI void comb_mul_g9(gej9& acc, bool& inf, const sc& u, const uint4* __restrict__ gtab) {
     inf = true;
     ge9 Pn;
-    gtab_load(Pn, gtab + (size_t)(u.v[0] & 0xFFu) * GTAB_ENTRY_U4);
+    gtab_load(Pn, gtab + (size_t)comb_digit(u, 0) * GTAB_ENTRY_U4);
 #pragma unroll 1
-    for (int w = 0; w < 32; w++) {
-        uint32_t d = (sel_word(u.v, (uint32_t)w >> 2) >> ((w & 3) * 8)) & 0xFFu;
+    for (int w = 0; w < COMB_WINDOWS; w++) {
+        uint32_t d = comb_digit(u, (uint32_t)w);
         ge9 P = Pn;
-        if (w < 31) {  // prefetch next window's entry
-            uint32_t dn = (sel_word(u.v, (uint32_t)(w + 1) >> 2) >> (((w + 1) & 3) * 8)) & 0xFFu;
-            gtab_load(Pn, gtab + ((size_t)(w + 1) * 256 + dn) * GTAB_ENTRY_U4);
+        if (w < COMB_WINDOWS - 1) {  // prefetch next window's entry
+            uint32_t dn = comb_digit(u, (uint32_t)w + 1);
+            gtab_load(Pn, gtab + (((size_t)(w + 1) << COMB_BITS) + dn) * GTAB_ENTRY_U4);
         }
         gej9 t;
         bool tinf = inf;
