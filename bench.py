@@ -471,6 +471,9 @@ def main():
                          "unit": "TMAC/s", "frac": round(achieved / PEAK_MAC, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": N_SIGS * (32 + 65 + 65 + 20 + 1),
+                         # by design: one 80-byte affine comb entry per 16-bit window of u1 (16 per
+                         # recovery) from the 80 MiB Infinity-Cache-resident table
+                         "comb_table_bytes_per_launch": N_SIGS * 16 * 80,
                          "kernel": "k_ecrecover", "kernel_avg_ms": round(k_avg_ms, 4),
                          "algorithmic_per_unit": f"{MACS_PER_RECOVERY} 32x32-bit partial products per recovery"},
             "cpu_baseline": cpu,
