@@ -703,26 +703,46 @@ struct TopLevels {
     int h0, h1;  // heights h0..h1 (inclusive), index h - 1 below
     int hb[TOP_MAX_H], he[TOP_MAX_H], gb[TOP_MAX_H], ge[TOP_MAX_H];
 };
-constexpr int TOP_BLOCK = 256;
-constexpr int TOP_WAVES = TOP_BLOCK / 64;
+constexpr int TOP_HFULL_THREADS = 256;  // waves 0-3: HFULL nodes, one per lane
+constexpr int TOP_GEN_WAVES = 2;        // waves 4-5: generic nodes, one per wave (never behind HFULL work)
+constexpr int TOP_BLOCK = TOP_HFULL_THREADS + 64 * TOP_GEN_WAVES;
 
-// one workgroup per body; per height: HFULL nodes one per lane, generic nodes one per wave (LDS
-// message buffers), a barrier between heights (children's hashes are in the CU's L1/L2)
+// one workgroup per body; per height: HFULL nodes one per lane of waves 0-3, generic nodes one per
+// wave of waves 4-5 (LDS message buffers) so a level's generic chain runs beside its HFULL nodes,
+// a barrier between heights (children's hashes are in the CU's L1/L2)
 __global__ __launch_bounds__(TOP_BLOCK) void k_chunk_top(const PNode* __restrict__ nodes,
                                                          const PChild* __restrict__ children, TopLevels tl,
                                                          BodyBatch bb) {
-    __shared__ uint64_t gbuf[TOP_WAVES * MSG_STRIDE / 8];
+    __shared__ uint64_t gbuf[TOP_GEN_WAVES * MSG_STRIDE / 8];
     uint32_t body = blockIdx.x;
-    int tid = threadIdx.x, wave = tid >> 6;
-    uint8_t* m = (uint8_t*)gbuf + wave * MSG_STRIDE;
+    int tid = threadIdx.x, gw = (tid - TOP_HFULL_THREADS) >> 6;  // generic wave index (tid >= 256)
+    uint8_t* m = (uint8_t*)gbuf + (gw >= 0 ? gw : 0) * MSG_STRIDE;
+#ifdef GSV_TOP_TRACE
+    uint64_t t_start = __builtin_amdgcn_s_memtime(), t_lv[TOP_MAX_H + 1];
+#endif
     for (int h = tl.h0; h <= tl.h1; h++) {
         int hb = tl.hb[h - 1], he = tl.he[h - 1];
-        for (int i = hb + tid; i < he; i += TOP_BLOCK) do_hfull(nodes[i], bb, body);
-        int gb = tl.gb[h - 1], ge = tl.ge[h - 1];
-        for (int i = gb + (TOP_WAVES - 1 - wave); i < ge; i += TOP_WAVES)
-            do_generic_wave(nodes[i], children, nodes, bb, body, m);
+        if (tid < TOP_HFULL_THREADS) {
+            for (int i = hb + tid; i < he; i += TOP_HFULL_THREADS) do_hfull(nodes[i], bb, body);
+        } else {
+            int gb = tl.gb[h - 1], ge = tl.ge[h - 1];
+            for (int i = gb + gw; i < ge; i += TOP_GEN_WAVES) do_generic_wave(nodes[i], children, nodes, bb, body, m);
+        }
         __syncthreads();
+#ifdef GSV_TOP_TRACE
+        t_lv[h] = __builtin_amdgcn_s_memtime();
+#endif
     }
+#ifdef GSV_TOP_TRACE
+    if (blockIdx.x == 0 && tid == 0) {
+        uint64_t prev = t_start;
+        for (int h = tl.h0; h <= tl.h1; h++) {
+            printf("top h=%d hfull=%d gen=%d ticks=%llu\n", h, tl.he[h - 1] - tl.hb[h - 1], tl.ge[h - 1] - tl.gb[h - 1],
+                   (unsigned long long)(t_lv[h] - prev));
+            prev = t_lv[h];
+        }
+    }
+#endif
 }
 
 // ================================================================ launcher
