@@ -346,6 +346,28 @@ static BN_NI void fp6_mul_p(fp6* e, const fp6* pa, const fp6* pb) {
     e->z = tz;
 }
 GSV_DI void fp6_mul(fp6& e, const fp6& a, const fp6& b) { fp6_mul_p(&e, &a, &b); }
+// e = a * (by tau + bz) (a line's sparse factor, x coefficient 0): 5 F_p^2 products instead of 6;
+// the same field element as fp6_mul with b.x = 0, hence the same canonical words.
+static BN_NI void fp6_mul_sparse_p(fp6* e, const fp6* pa, const fp2* pby, const fp2* pbz) {
+    const fp6 a = *pa;
+    const fp2 by = *pby, bz = *pbz;
+    fp2 v0, v1, t0, t1, tx, ty, tz;
+    fp2_mul(v0, a.z, bz);
+    fp2_mul(v1, a.y, by);
+    fp2_mul(tz, a.x, by);  // tau^3 = xi
+    fp2_mul_xi(tz, tz);
+    fp2_add(tz, tz, v0);
+    fp2_add(t0, a.y, a.z);
+    fp2_add(t1, by, bz);
+    fp2_mul(ty, t0, t1);
+    fp2_sub(ty, ty, v0);
+    fp2_sub(ty, ty, v1);
+    fp2_mul(tx, a.x, bz);
+    fp2_add(tx, tx, v1);
+    e->x = tx;
+    e->y = ty;
+    e->z = tz;
+}
 static BN_NI void fp6_mul_fp2_p(fp6* e, const fp6* a, const fp2* b) {
     fp2_mul(e->x, a->x, *b);
     fp2_mul(e->y, a->y, *b);

@@ -410,17 +410,13 @@ static BN_NI void line_double_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g1a* p
 GSV_DI void line_double(fp2& a, fp2& b, fp2& c, g2j& r, const g1a& q) { line_double_p(&a, &b, &c, &r, &q); }
 // optate.go:94-112
 static BN_NI void mul_line(fp12* ret, const fp2* a, const fp2* b, const fp2* c) {
-    fp6 a2, t3, t2, rx;
-    fp2_zero(a2.x);
-    a2.y = *a;
-    a2.z = *b;
-    fp6_mul(a2, a2, ret->x);
+    fp6 a2, t3, rx;
+    fp2 bc;
+    fp6_mul_sparse_p(&a2, &ret->x, a, b);  // (0, a, b) * ret.x
     fp6_mul_fp2(t3, ret->y, *c);
-    fp2_zero(t2.x);
-    t2.y = *a;
-    fp2_add(t2.z, *b, *c);
+    fp2_add(bc, *b, *c);
     fp6_add(rx, ret->x, ret->y);
-    fp6_mul(rx, rx, t2);
+    fp6_mul_sparse_p(&rx, &rx, a, &bc);  // * (0, a, b + c)
     fp6_sub(rx, rx, a2);
     fp6_sub(rx, rx, t3);
     ret->x = rx;
@@ -671,13 +667,18 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ c
             uint32_t j = pidx[q];
             if (pstat[j] != PS_OK) continue;
             g1a P;
-            g2a Q;
-            pts_load(P, Q, pts, npairs, j);
+            soa_load(P.x, pts, npairs, j, 0);
+            soa_load(P.y, pts, npairs, j, 1);
             g2j r;
             g2j_load(r, rs, npairs, j);
             line_double(la, lb, lc, r, P);
             mul_line(&f, &la, &lb, &lc);
-            if (add) {
+            if (add) {  // Q is only needed on the NAF's nonzero digits
+                g2a Q;
+                soa_load(Q.x.x, pts, npairs, j, 2);
+                soa_load(Q.x.y, pts, npairs, j, 3);
+                soa_load(Q.y.x, pts, npairs, j, 4);
+                soa_load(Q.y.y, pts, npairs, j, 5);
                 fp2 r2;
                 fp2_sqr(r2, Q.y);
                 if (NAF_NEG & bit) fp2_neg(Q.y, Q.y);
