@@ -598,6 +598,61 @@ GSV_DI void write_child(Writer& w, const BodyBatch& bb, uint32_t body, const PCh
     else copy_ref(w, child_slot(bb, body, c, nodes));
 }
 
+// One generic node assembled and hashed by one lane in the node's own HBM message buffer (msg_off):
+// the throughput form, for heights with many generic nodes (every height of a generic DeriveSha
+// plan over a large batch), where a wave per node would idle 63 lanes through the permutations.
+GSV_DI void do_generic_lane(const PNode& nd, const PChild* __restrict__ children, const PNode* __restrict__ nodes,
+                            const BodyBatch& bb, uint32_t body) {
+    const PChild* ch = nd.child_begin >= 0 ? children + nd.child_begin : nullptr;
+    uint8_t* m = bb.msg + (size_t)body * bb.msg_stride + nd.msg_off;
+    uint8_t ck[8];
+    int cl = 0;
+    uint32_t plen;
+    if (nd.kind == PK_BRANCH) {
+        plen = 1 + (16 - nd.nchild);
+        for (int k = 0; k < nd.nchild; k++) plen += child_len(bb, body, ch[k], nodes);
+    } else if (nd.kind == PK_EXT) {
+        cl = compact_key(ck, nd.first_i, nd.depth, nd.ext_end);
+        plen = str_len(ck, cl) + child_len(bb, body, ch[0], nodes);
+    } else {
+        cl = compact_key(ck, nd.first_i, nd.depth, key_len(nd.first_i));
+        plen = str_len(ck, cl) + byte_val_len(bb.bodies[bb.body_off[body] + nd.first_i]);
+    }
+    Writer w{m, 0};
+    w.list_header(plen);
+    if (nd.kind == PK_BRANCH) {
+        int k = 0;
+        for (int slot = 0; slot < 16; slot++) {
+            if (k < nd.nchild && ch[k].slot == slot) {
+                write_child(w, bb, body, ch[k], nodes);
+                k++;
+            } else {
+                w.put(0x80);
+            }
+        }
+        w.put(0x80);
+    } else if (nd.kind == PK_EXT) {
+        w.str(ck, cl);
+        write_child(w, bb, body, ch[0], nodes);
+    } else {
+        w.str(ck, cl);
+        put_byte_val(w, bb.bodies[bb.body_off[body] + nd.first_i]);
+    }
+    uint32_t len = w.n;
+    if (len >= 32 || nd.is_root) {
+        uint32_t h[8];
+        keccak_buf(h, m, len);
+        emit_hash(nd, bb, body, h);
+    } else {
+        uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE;
+        s[0] = (uint8_t)len;
+        for (uint32_t k = 0; k < len; k++) s[8 + k] = m[k];
+    }
+}
+
+// generic nodes of one height, over all bodies, above which one lane per node beats one wave per node
+constexpr uint64_t GEN_LANE_MODE_MIN = 4096;
+
 // One generic node (BRANCH / EXT / byte-mode root LEAF), assembled by a whole wave: lane k writes
 // piece k of the RLP payload (BRANCH: slots 0..15 + the value slot; EXT / LEAF: key, child/value)
 // at an offset from a wave prefix sum into the wave's LDS buffer m (8-byte aligned, MSG_STRIDE
@@ -675,6 +730,7 @@ struct LevelLaunch {
     int n0, nn;  // BOTTOM (BOT) or HFULL (!BOT) node range
     int g0, ng;  // generic node range
     uint32_t gen_blocks;
+    int gen_lane;  // 1: one generic node per lane (gen_blocks of 256 lanes), 0: one per wave
 };
 template <bool BOT>
 __global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ nodes,
@@ -682,6 +738,13 @@ __global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ n
                                                      BodyBatch bb) {
     __shared__ uint64_t sbuf[(BOT ? 256 * BOT_BUF : 4 * MSG_STRIDE) / 8];
     uint32_t blk = blockIdx.x;
+    if (blk < L.gen_blocks && L.gen_lane) {
+        uint64_t t = (uint64_t)blk * 256 + threadIdx.x;
+        if (t >= (uint64_t)L.ng * bb.nbodies) return;
+        const PNode nd = nodes[L.g0 + (int)(t % (uint64_t)L.ng)];
+        do_generic_lane(nd, children, nodes, bb, (uint32_t)(t / (uint64_t)L.ng));
+        return;
+    }
     if (blk < L.gen_blocks) {
         uint64_t w = (uint64_t)blk * 4 + (threadIdx.x >> 6);
         if (w >= (uint64_t)L.ng * bb.nbodies) return;  // uniform per wave
@@ -702,7 +765,9 @@ __global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ n
 struct TopLevels {
     int h0, h1;  // heights h0..h1 (inclusive), index h - 1 below
     int hb[TOP_MAX_H], he[TOP_MAX_H], gb[TOP_MAX_H], ge[TOP_MAX_H];
+    uint32_t gen_lane;  // bit h - 1: that height's generic nodes one per lane (throughput form)
 };
+constexpr uint32_t TOP_MAX_BODIES = 256;  // one fused-top workgroup per CU at most
 constexpr int TOP_HFULL_THREADS = 256;  // waves 0-3: HFULL nodes, one per lane
 constexpr int TOP_GEN_WAVES = 2;        // waves 4-5: generic nodes, one per wave (never behind HFULL work)
 constexpr int TOP_BLOCK = TOP_HFULL_THREADS + 64 * TOP_GEN_WAVES;
@@ -713,20 +778,29 @@ constexpr int TOP_BLOCK = TOP_HFULL_THREADS + 64 * TOP_GEN_WAVES;
 __global__ __launch_bounds__(TOP_BLOCK) void k_chunk_top(const PNode* __restrict__ nodes,
                                                          const PChild* __restrict__ children, TopLevels tl,
                                                          BodyBatch bb) {
-    __shared__ uint64_t gbuf[TOP_GEN_WAVES * MSG_STRIDE / 8];
+    __shared__ uint64_t gbuf[(TOP_BLOCK / 64) * MSG_STRIDE / 8];
     uint32_t body = blockIdx.x;
-    int tid = threadIdx.x, gw = (tid - TOP_HFULL_THREADS) >> 6;  // generic wave index (tid >= 256)
-    uint8_t* m = (uint8_t*)gbuf + (gw >= 0 ? gw : 0) * MSG_STRIDE;
+    int tid = threadIdx.x, wave = tid >> 6;
+    uint8_t* m = (uint8_t*)gbuf + wave * MSG_STRIDE;
 #ifdef GSV_TOP_TRACE
     uint64_t t_start = __builtin_amdgcn_s_memtime(), t_lv[TOP_MAX_H + 1];
 #endif
     for (int h = tl.h0; h <= tl.h1; h++) {
         int hb = tl.hb[h - 1], he = tl.he[h - 1];
-        if (tid < TOP_HFULL_THREADS) {
-            for (int i = hb + tid; i < he; i += TOP_HFULL_THREADS) do_hfull(nodes[i], bb, body);
-        } else {
-            int gb = tl.gb[h - 1], ge = tl.ge[h - 1];
-            for (int i = gb + gw; i < ge; i += TOP_GEN_WAVES) do_generic_wave(nodes[i], children, nodes, bb, body, m);
+        int gb = tl.gb[h - 1], ge = tl.ge[h - 1];
+        if ((tl.gen_lane >> (h - 1)) & 1u) {  // many generic nodes: one per lane, after the HFULL lanes
+            for (int i = hb + tid; i < he; i += TOP_BLOCK) do_hfull(nodes[i], bb, body);
+            for (int i = gb + tid; i < ge; i += TOP_BLOCK) do_generic_lane(nodes[i], children, nodes, bb, body);
+        } else if (he > hb) {  // HFULL nodes on waves 0-3, generic nodes on waves 4-5
+            if (tid < TOP_HFULL_THREADS) {
+                for (int i = hb + tid; i < he; i += TOP_HFULL_THREADS) do_hfull(nodes[i], bb, body);
+            } else {
+                int gw = wave - TOP_HFULL_THREADS / 64;
+                for (int i = gb + gw; i < ge; i += TOP_GEN_WAVES)
+                    do_generic_wave(nodes[i], children, nodes, bb, body, m);
+            }
+        } else {  // generic-only height (all of a generic DeriveSha plan): every wave takes nodes
+            for (int i = gb + wave; i < ge; i += TOP_BLOCK / 64) do_generic_wave(nodes[i], children, nodes, bb, body, m);
         }
         __syncthreads();
 #ifdef GSV_TOP_TRACE
@@ -757,7 +831,10 @@ static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipSt
                                 void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx) {
     const TriePlanHost& p = plan->h;
     uint32_t nb = bb.nbodies;
-    for (int h = 1; h < p.top_h; h++) {
+    // the fused top is a latency tool: one workgroup per body, so it only pays while the bodies fit
+    // on the CUs at once; a larger batch runs every height as a dense per-height launch instead
+    const int top_h = nb <= TOP_MAX_BODIES ? p.top_h : p.height + 1;
+    for (int h = 1; h < top_h; h++) {
         int b0 = p.lvl_bottom_begin[h - 1], b1 = p.lvl_bottom_end[h - 1];
         int f0 = p.lvl_hfull_begin[h - 1], f1 = p.lvl_hfull_end[h - 1];
         int g0 = p.lvl_gen_begin[h - 1], g1 = p.lvl_gen_end[h - 1];
@@ -767,7 +844,8 @@ static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipSt
         L.nn = bot ? b1 - b0 : f1 - f0;
         L.g0 = g0;
         L.ng = g1 - g0;
-        L.gen_blocks = (uint32_t)(((uint64_t)L.ng * nb + 3) / 4);
+        L.gen_lane = (uint64_t)L.ng * nb >= GEN_LANE_MODE_MIN ? 1 : 0;
+        L.gen_blocks = (uint32_t)(((uint64_t)L.ng * nb + (L.gen_lane ? 255 : 3)) / (L.gen_lane ? 256 : 4));
         uint64_t blocks = L.gen_blocks + ((uint64_t)L.nn * nb + 255) / 256;
         if (blocks == 0) continue;
         int kid = bot ? GSV_K_CHUNK_LEAF : GSV_K_CHUNK_LEVEL;
@@ -782,16 +860,17 @@ static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipSt
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    if (p.top_h <= p.height) {
+    if (top_h <= p.height) {
         if (p.height > TOP_MAX_H) return hipErrorInvalidValue;
         TopLevels tl{};
-        tl.h0 = p.top_h;
+        tl.h0 = top_h;
         tl.h1 = p.height;
         for (int h = 1; h <= p.height; h++) {
             tl.hb[h - 1] = p.lvl_hfull_begin[h - 1];
             tl.he[h - 1] = p.lvl_hfull_end[h - 1];
             tl.gb[h - 1] = p.lvl_gen_begin[h - 1];
             tl.ge[h - 1] = p.lvl_gen_end[h - 1];
+            if ((uint64_t)(tl.ge[h - 1] - tl.gb[h - 1]) * nb >= GEN_LANE_MODE_MIN) tl.gen_lane |= 1u << (h - 1);
         }
         if (timer_begin) timer_begin(tctx, GSV_K_CHUNK_LEVEL);
         hipLaunchKernelGGL(k_chunk_top, dim3(nb), dim3(TOP_BLOCK), 0, st, plan->d_nodes, plan->d_children, tl, bb);
@@ -843,7 +922,7 @@ GSV_DI uint32_t prefix_len(uint32_t len) {
 // parent when the RLP is < 32 bytes, else hashed; a list of one item is that leaf, hashed as root.
 __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__ vals,
                                                      const uint64_t* __restrict__ voff,
-                                                     const uint64_t* __restrict__ lmsg_off, uint8_t* lmsg,
+                                                     uint8_t* lmsg,
                                                      const uint64_t* __restrict__ leaf_base,
                                                      const uint16_t* __restrict__ leaf_depth, uint32_t N,
                                                      uint32_t nlists, uint8_t* leafrefs, uint8_t* roots) {
@@ -859,7 +938,9 @@ __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__
     uint32_t kenc = (cl == 1 && ck[0] < 0x80) ? 1u : 1u + cl;
     bool vbyte = (L == 1 && v[0] < 0x80);
     uint32_t venc = vbyte ? 1u : prefix_len(L) + L;
-    uint8_t* m = lmsg + lmsg_off[item];
+    // this item's message buffer: 8-byte aligned, disjoint from its neighbours' (each needs <= L + 17
+    // bytes and starts at least L + 25 bytes after the previous one)
+    uint8_t* m = lmsg + (((voff[item] - voff[0]) + 7) & ~7ull) + 32ull * item;
     Writer w{m, 0};
     put_prefix(w, 0xc0, kenc + venc);
     w.str(ck, cl);
@@ -887,8 +968,7 @@ size_t derive_sha_scratch_bytes(const TriePlan* plan, uint32_t nlists) {
 }
 
 hipError_t launch_derive_sha_plan(const TriePlan* plan, uint32_t nlists, const uint8_t* d_vals,
-                                  const uint64_t* d_voff, const uint64_t* d_leaf_base, const uint64_t* d_lmsg_off,
-                                  uint8_t* d_lmsg, uint8_t* d_leafrefs, uint8_t* d_scratch, uint8_t* d_roots,
+                                  const uint64_t* d_voff, const uint64_t* d_leaf_base, uint8_t* d_lmsg, uint8_t* d_leafrefs, uint8_t* d_scratch, uint8_t* d_roots,
                                   hipStream_t st, void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
                                   void* tctx) {
     const TriePlanHost& p = plan->h;
@@ -896,7 +976,7 @@ hipError_t launch_derive_sha_plan(const TriePlan* plan, uint32_t nlists, const u
     uint64_t total = (uint64_t)p.N * nlists;
     if (timer_begin) timer_begin(tctx, GSV_K_DERIVE_LEAF);
     hipLaunchKernelGGL(k_derive_leaf, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d_vals, d_voff,
-                       d_lmsg_off, d_lmsg, d_leaf_base, plan->d_leaf_depth, p.N, nlists, d_leafrefs, d_roots);
+                       d_lmsg, d_leaf_base, plan->d_leaf_depth, p.N, nlists, d_leafrefs, d_roots);
     if (timer_end) timer_end(tctx, GSV_K_DERIVE_LEAF);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.nodes.empty()) return e;

@@ -933,13 +933,9 @@ static int derive_sha_dev_impl(gsv_ctx* c, const uint8_t* d_vals, const uint64_t
     for (uint64_t k = list_off[0]; k < list_off[n]; k++)
         if (voff[k + 1] < voff[k] || voff[k + 1] - voff[k] >= (1ull << 32)) return GSV_E_INVALID_ARG;
     // per item: message buffer offset (8-aligned, value + 24 bytes of RLP headers) and ref slot
-    std::vector<uint64_t> lmsg(total + 1);
-    uint64_t pos = 0;
-    for (uint64_t k = 0; k < total; k++) {
-        lmsg[k] = pos;
-        pos += (voff[list_off[0] + k + 1] - voff[list_off[0] + k] + 24 + 7) & ~7ull;
-    }
-    size_t need = al((total + 1) * 8) * 2 + al(pos + 256) + al(total * 48);
+    // per-item leaf message buffers are placed by the kernel (k_derive_leaf): aligned bytes + 32 per item
+    uint64_t pos = ((voff[list_off[n]] - voff[list_off[0]] + 7) & ~7ull) + 32ull * total;
+    size_t need = al((total + 1) * 8) + al(pos + 256) + al(total * 48);
     for (auto& g : groups) {
         if (g.first == 0) continue;
         gsv::TriePlan* pl = c->plans.get((uint32_t)g.first, true);
@@ -954,11 +950,9 @@ static int derive_sha_dev_impl(gsv_ctx* c, const uint8_t* d_vals, const uint64_t
     c->cur_stream = st;
     // voff rebased to d_vals is what the caller gave; items indexed from list_off[0]
     uint64_t* d_voff = cv.take<uint64_t>((total + 1) * 8);
-    uint64_t* d_lmsg_off = cv.take<uint64_t>((total + 1) * 8);
     uint8_t* d_lmsg = cv.take<uint8_t>(pos + 256);
     uint8_t* d_leafrefs = cv.take<uint8_t>(total * 48);
     HIPCHK(hipMemcpyAsync(d_voff, voff + list_off[0], (total + 1) * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_lmsg_off, lmsg.data(), (total + 1) * 8, hipMemcpyHostToDevice, st));
     std::vector<std::vector<uint64_t>> host_base;
     host_base.reserve(groups.size());
     for (auto& g : groups) {
@@ -976,7 +970,7 @@ static int derive_sha_dev_impl(gsv_ctx* c, const uint8_t* d_vals, const uint64_t
         auto& hb = host_base.back();
         for (size_t k = 0; k < idx.size(); k++) hb[k] = list_off[idx[k]] - list_off[0];
         HIPCHK(hipMemcpyAsync(d_base, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(gsv::launch_derive_sha_plan(pl, (uint32_t)idx.size(), d_vals, d_voff, d_base, d_lmsg_off, d_lmsg,
+        HIPCHK(gsv::launch_derive_sha_plan(pl, (uint32_t)idx.size(), d_vals, d_voff, d_base, d_lmsg,
                                            d_leafrefs, d_scr, d_gr, st, hook_begin, hook_end, c));
         size_t k = 0;
         while (k < idx.size()) {
