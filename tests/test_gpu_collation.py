@@ -157,3 +157,37 @@ def test_sharding_mirror_api(ctx, oracle):
     assert poc.hex() == golden("collation.json")["poc"][0]["poc"]
     assert S.DeriveSha([bytes.fromhex(x) for x in golden("trie.json")["derive_sha"][0]["items"]]).hex() == \
         golden("trie.json")["derive_sha"][0]["root"]
+
+
+def test_dev_calls_on_two_streams_share_the_workspace_safely(ctx, oracle):
+    # *_dev calls return without a host sync; calls on different streams are ordered on the GPU
+    # through the context's workspace event (gsv_api.hip work_begin/work_end)
+    import torch
+    rng = np.random.default_rng(17)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    sizes = [[70000, 3000, 129], [4096, 1 << 16], [17, 300000, 5, 1]]
+    jobs = []
+    for k, sz in enumerate(sizes):
+        bodies = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sz]
+        off = np.zeros(len(bodies) + 1, np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bodies])
+        dev = torch.tensor(np.frombuffer(b"".join(bodies), np.uint8).copy(), device="cuda")
+        roots = torch.zeros((len(bodies), 32), dtype=torch.uint8, device="cuda")
+        st = s1 if k % 2 == 0 else s2
+        ctx.chunk_root_batch_dev(dev, off, roots, stream=st)
+        jobs.append((bodies, roots, dev))
+    salt = bytes(range(3, 23))
+    pb = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in [1000, 0, 64]]
+    poff = np.zeros(4, np.uint64)
+    poff[1:] = np.cumsum([len(b) for b in pb])
+    pdev = torch.tensor(np.frombuffer(b"".join(pb) + b"\0", np.uint8).copy(), device="cuda")
+    pocs = torch.zeros((3, 32), dtype=torch.uint8, device="cuda")
+    ctx.collation_poc_batch_dev(pdev, poff, salt, pocs, stream=s2)
+    torch.cuda.synchronize()
+    for bodies, roots, _ in jobs:
+        r = roots.cpu().numpy()
+        for i, b in enumerate(bodies):
+            assert bytes(r[i]) == oracle.derive_sha_bytes(b), (len(b), i)
+    p = pocs.cpu().numpy()
+    for i, b in enumerate(pb):
+        assert bytes(p[i]) == oracle.calculate_poc(b, salt), i
