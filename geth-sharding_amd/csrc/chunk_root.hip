@@ -653,14 +653,21 @@ GSV_DI void do_generic_lane(const PNode& nd, const PChild* __restrict__ children
 // generic nodes of one height, over all bodies, above which one lane per node beats one wave per node
 constexpr uint64_t GEN_LANE_MODE_MIN = 4096;
 
-// One generic node (BRANCH / EXT / byte-mode root LEAF), assembled by a whole wave: lane k writes
-// piece k of the RLP payload (BRANCH: slots 0..15 + the value slot; EXT / LEAF: key, child/value)
-// at an offset from a wave prefix sum into the wave's LDS buffer m (8-byte aligned, MSG_STRIDE
-// bytes), so the ≤16 child-ref loads are issued in parallel; lane 0 then hashes (>= 32 bytes or
-// root, trie/hasher.go:163) or inlines the RLP into the node's ref slot.  All 64 lanes must call.
-GSV_DI void do_generic_wave(const PNode& nd, const PChild* __restrict__ children, const PNode* __restrict__ nodes,
-                            const BodyBatch& bb, uint32_t body, uint8_t* m) {
-    const int lane = threadIdx.x & 63;
+// Generic node (BRANCH / EXT / byte-mode root LEAF) handled by a 32-lane group: lane k writes
+// payload piece k of the RLP (BRANCH: slots 0..15 + the value slot; EXT / LEAF: key, child/value)
+// at an offset from a group prefix sum into the group's LDS buffer m (8-byte aligned, MSG_STRIDE
+// bytes), so the <= 16 child-ref loads run in parallel; the group then hashes it with the
+// cooperative Keccak (>= 32 bytes or root, trie/hasher.go:163) or lane 0 inlines the RLP into the
+// node's ref slot.  All 32 lanes of the group must call, with the same node.
+GSV_DI void group_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+GSV_DI void do_generic_group(const PNode& nd, const PChild* __restrict__ children, const PNode* __restrict__ nodes,
+                             const BodyBatch& bb, uint32_t body, uint8_t* m) {
+    const int lane = threadIdx.x & 31;
     const PChild* ch = nd.child_begin >= 0 ? children + nd.child_begin : nullptr;
     // this lane's piece: 0 none, 1 empty slot / value slot (0x80), 2 child, 3 key, 4 byte value
     int piece = 0;
@@ -691,11 +698,11 @@ GSV_DI void do_generic_wave(const PNode& nd, const PChild* __restrict__ children
                   : piece == 3 ? str_len(ck, cl) : piece == 4 ? byte_val_len(bval) : 0u;
     uint32_t incl = plen;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t v = __shfl_up(incl, d, 64);
+    for (int d = 1; d < 32; d <<= 1) {
+        uint32_t v = __shfl_up(incl, d, 32);
         if (lane >= d) incl += v;
     }
-    uint32_t total = __shfl(incl, 63, 64);
+    uint32_t total = __shfl(incl, 31, 32);
     uint32_t hl = total < 56 ? 1u : total < 256 ? 2u : 3u;
     Writer w{m, hl + incl - plen};
     if (piece == 1) w.put(0x80);
@@ -706,21 +713,43 @@ GSV_DI void do_generic_wave(const PNode& nd, const PChild* __restrict__ children
         Writer hw{m, 0};
         hw.list_header(total);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    group_sync();
     uint32_t len = hl + total;
-    if (lane == 0) {
-        if (len >= 32 || nd.is_root) {
-            uint32_t h[8];
-            keccak_buf(h, m, len);
-            emit_hash(nd, bb, body, h);
-        } else {
-            uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE;
-            s[0] = (uint8_t)len;
-            for (uint32_t k = 0; k < len; k++) s[8 + k] = m[k];
-        }
+    if (len >= 32 || nd.is_root) {
+        uint32_t h[8];
+        keccak256_coop(h, m, len, lane);
+        if (lane == 0) emit_hash(nd, bb, body, h);
+    } else if (lane == 0) {
+        uint8_t* s = bb.refs + (size_t)body * bb.ref_stride + (size_t)nd.ref_slot * REF_STRIDE;
+        s[0] = (uint8_t)len;
+        for (uint32_t k = 0; k < len; k++) s[8 + k] = m[k];
     }
+    group_sync();  // m is reused by the group's next node
+}
+
+// HFULL node by a 32-lane group: the 532-byte message is laid out in LDS (lanes 0..15 copy child
+// hash s after its a0 byte, lane 16 the list header and value slot), then hashed cooperatively
+GSV_DI void do_hfull_group(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8_t* m) {
+    const int lane = threadIdx.x & 31;
+    const uint4* H = (const uint4*)(bb.msg + (size_t)body * bb.msg_stride + nd.msg_off);
+    if (lane < 16) {
+        uint4 a = H[2 * lane], b = H[2 * lane + 1];
+        uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint8_t* d = m + 3 + 33 * lane;
+        d[0] = 0xa0;
+#pragma unroll
+        for (int k = 0; k < 32; k++) d[1 + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    } else if (lane == 16) {
+        m[0] = 0xf9;
+        m[1] = 0x02;
+        m[2] = 0x11;
+        m[531] = 0x80;
+    }
+    group_sync();
+    uint32_t h[8];
+    keccak256_coop(h, m, 532, lane);
+    if (lane == 0) emit_hash(nd, bb, body, h);
+    group_sync();
 }
 
 // One height below the fused top: generic nodes (one wave each) in the first gen_blocks workgroups
@@ -736,7 +765,7 @@ template <bool BOT>
 __global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ nodes,
                                                      const PChild* __restrict__ children, LevelLaunch L,
                                                      BodyBatch bb) {
-    __shared__ uint64_t sbuf[(BOT ? 256 * BOT_BUF : 4 * MSG_STRIDE) / 8];
+    __shared__ uint64_t sbuf[(BOT ? 256 * BOT_BUF : 8 * MSG_STRIDE) / 8];
     uint32_t blk = blockIdx.x;
     if (blk < L.gen_blocks && L.gen_lane) {
         uint64_t t = (uint64_t)blk * 256 + threadIdx.x;
@@ -746,11 +775,11 @@ __global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ n
         return;
     }
     if (blk < L.gen_blocks) {
-        uint64_t w = (uint64_t)blk * 4 + (threadIdx.x >> 6);
-        if (w >= (uint64_t)L.ng * bb.nbodies) return;  // uniform per wave
-        uint32_t body = (uint32_t)(w / (uint64_t)L.ng);
-        const PNode nd = nodes[L.g0 + (int)(w % (uint64_t)L.ng)];
-        do_generic_wave(nd, children, nodes, bb, body, (uint8_t*)sbuf + (threadIdx.x >> 6) * MSG_STRIDE);
+        uint64_t g = (uint64_t)blk * 8 + (threadIdx.x >> 5);  // one node per 32-lane group
+        if (g >= (uint64_t)L.ng * bb.nbodies) return;         // uniform per group
+        uint32_t body = (uint32_t)(g / (uint64_t)L.ng);
+        const PNode nd = nodes[L.g0 + (int)(g % (uint64_t)L.ng)];
+        do_generic_group(nd, children, nodes, bb, body, (uint8_t*)sbuf + (threadIdx.x >> 5) * MSG_STRIDE);
         return;
     }
     uint64_t t = (uint64_t)(blk - L.gen_blocks) * 256 + threadIdx.x;
@@ -772,35 +801,43 @@ constexpr int TOP_HFULL_THREADS = 256;  // waves 0-3: HFULL nodes, one per lane
 constexpr int TOP_GEN_WAVES = 2;        // waves 4-5: generic nodes, one per wave (never behind HFULL work)
 constexpr int TOP_BLOCK = TOP_HFULL_THREADS + 64 * TOP_GEN_WAVES;
 
-// one workgroup per body; per height: HFULL nodes one per lane of waves 0-3, generic nodes one per
-// wave of waves 4-5 (LDS message buffers) so a level's generic chain runs beside its HFULL nodes,
-// a barrier between heights (children's hashes are in the CU's L1/L2)
+// one workgroup per body, a barrier between heights (children's hashes are in the CU's L1/L2).
+// Per height: many HFULL nodes -> one per lane of waves 0-3 while the generic nodes go to the
+// 32-lane groups of waves 4-5; few nodes (the chain up to the root) -> every node to a 32-lane group
+// and the cooperative Keccak, which cuts each permutation's latency about threefold.
+constexpr int TOP_GROUPS = TOP_BLOCK / 32;
+constexpr int TOP_COOP_MAX = TOP_GROUPS;  // nodes per height up to which every node is group-hashed (one round)
+
 __global__ __launch_bounds__(TOP_BLOCK) void k_chunk_top(const PNode* __restrict__ nodes,
                                                          const PChild* __restrict__ children, TopLevels tl,
                                                          BodyBatch bb) {
-    __shared__ uint64_t gbuf[(TOP_BLOCK / 64) * MSG_STRIDE / 8];
+    __shared__ uint64_t gbuf[TOP_GROUPS * MSG_STRIDE / 8];
     uint32_t body = blockIdx.x;
-    int tid = threadIdx.x, wave = tid >> 6;
-    uint8_t* m = (uint8_t*)gbuf + wave * MSG_STRIDE;
+    int tid = threadIdx.x, grp = tid >> 5;
+    uint8_t* m = (uint8_t*)gbuf + grp * MSG_STRIDE;
 #ifdef GSV_TOP_TRACE
     uint64_t t_start = __builtin_amdgcn_s_memtime(), t_lv[TOP_MAX_H + 1];
 #endif
     for (int h = tl.h0; h <= tl.h1; h++) {
         int hb = tl.hb[h - 1], he = tl.he[h - 1];
         int gb = tl.gb[h - 1], ge = tl.ge[h - 1];
+        int nh = he - hb, ng = ge - gb;
         if ((tl.gen_lane >> (h - 1)) & 1u) {  // many generic nodes: one per lane, after the HFULL lanes
             for (int i = hb + tid; i < he; i += TOP_BLOCK) do_hfull(nodes[i], bb, body);
             for (int i = gb + tid; i < ge; i += TOP_BLOCK) do_generic_lane(nodes[i], children, nodes, bb, body);
-        } else if (he > hb) {  // HFULL nodes on waves 0-3, generic nodes on waves 4-5
+        } else if (nh + ng <= TOP_COOP_MAX) {  // the latency chain: every node to a group
+            for (int k = grp; k < nh + ng; k += TOP_GROUPS) {
+                if (k < nh) do_hfull_group(nodes[hb + k], bb, body, m);
+                else do_generic_group(nodes[gb + k - nh], children, nodes, bb, body, m);
+            }
+        } else {  // HFULL nodes one per lane on waves 0-3, generic nodes on the groups of waves 4-5
             if (tid < TOP_HFULL_THREADS) {
                 for (int i = hb + tid; i < he; i += TOP_HFULL_THREADS) do_hfull(nodes[i], bb, body);
             } else {
-                int gw = wave - TOP_HFULL_THREADS / 64;
-                for (int i = gb + gw; i < ge; i += TOP_GEN_WAVES)
-                    do_generic_wave(nodes[i], children, nodes, bb, body, m);
+                int g = grp - TOP_HFULL_THREADS / 32;
+                for (int i = gb + g; i < ge; i += TOP_GROUPS - TOP_HFULL_THREADS / 32)
+                    do_generic_group(nodes[i], children, nodes, bb, body, m);
             }
-        } else {  // generic-only height (all of a generic DeriveSha plan): every wave takes nodes
-            for (int i = gb + wave; i < ge; i += TOP_BLOCK / 64) do_generic_wave(nodes[i], children, nodes, bb, body, m);
         }
         __syncthreads();
 #ifdef GSV_TOP_TRACE
@@ -845,7 +882,7 @@ static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipSt
         L.g0 = g0;
         L.ng = g1 - g0;
         L.gen_lane = (uint64_t)L.ng * nb >= GEN_LANE_MODE_MIN ? 1 : 0;
-        L.gen_blocks = (uint32_t)(((uint64_t)L.ng * nb + (L.gen_lane ? 255 : 3)) / (L.gen_lane ? 256 : 4));
+        L.gen_blocks = (uint32_t)(((uint64_t)L.ng * nb + (L.gen_lane ? 255 : 7)) / (L.gen_lane ? 256 : 8));
         uint64_t blocks = L.gen_blocks + ((uint64_t)L.nn * nb + 255) / 256;
         if (blocks == 0) continue;
         int kid = bot ? GSV_K_CHUNK_LEAF : GSV_K_CHUNK_LEVEL;

@@ -105,6 +105,81 @@ GSV_DI void keccakf(uint64_t a[25]) {
     for (int k = 0; k < 25; k++) a[k] = (uint64_t)al[k] | ((uint64_t)ah[k] << 32);
 }
 
+// ---------------------------------------------------------------- group-cooperative Keccak-f
+// Keccak-f[1600] by a 32-lane group (a half wave): lane i < 25 holds A[i] (x = i % 5, y = i / 5)
+// as (lo, hi); lanes 25..31 mirror lane 24 and are never read.  Column parities, the theta D
+// term, pi and chi's neighbours move between lanes with ds_bpermute (__shfl): 18 per round, so
+// one permutation's latency is ~3x shorter than one lane's 190-instruction rounds.  For the
+// latency-bound top of a trie, where one node at a time is on the critical path.
+__device__ constexpr int KECCAK_RHO_C[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
+                                             25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
+GSV_DI uint32_t gshfl(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 32); }
+
+GSV_DI void keccakf_coop(uint32_t& lo, uint32_t& hi, int i) {
+    const int x = i % 5, y = i / 5;
+    const int c1 = (i + 5) % 25, c2 = (i + 10) % 25, c3 = (i + 15) % 25, c4 = (i + 20) % 25;
+    const int xm = (x + 4) % 5, xp = (x + 1) % 5;
+    // pi: B[y + 5((2x + 3y) mod 5)] = rot(A[x + 5y]): lane (x, y) receives from (3(y - 3x) mod 5, x)
+    const int src = (3 * (((y - 3 * x) % 5 + 5) % 5)) % 5 + 5 * x;
+    const int n1 = (x + 1) % 5 + 5 * y, n2 = (x + 2) % 5 + 5 * y;
+    const int r = KECCAK_RHO_C[i];
+    const bool swap = (r & 32) != 0;
+    const uint32_t sh = 32u - (uint32_t)(r & 31);  // alignbit amount (r & 31 == 0 -> no rotate)
+    const bool rot = (r & 31) != 0;
+#pragma unroll 1
+    for (int round = 0; round < 24; round++) {
+        uint32_t cl = kxor3(kxor3(lo, gshfl(lo, c1), gshfl(lo, c2)), gshfl(lo, c3), gshfl(lo, c4));
+        uint32_t ch = kxor3(kxor3(hi, gshfl(hi, c1), gshfl(hi, c2)), gshfl(hi, c3), gshfl(hi, c4));
+        uint32_t ml = gshfl(cl, xm), mh = gshfl(ch, xm), pl = gshfl(cl, xp), ph = gshfl(ch, xp);
+        uint32_t rl, rh;
+        krot<1>(rl, rh, pl, ph);
+        uint32_t al = lo ^ ml ^ rl, ah = hi ^ mh ^ rh;
+        // rho: rotate by r (r >= 32: swap halves, then by r - 32)
+        uint32_t tl = swap ? ah : al, th = swap ? al : ah;
+        uint32_t ol = rot ? __builtin_amdgcn_alignbit(tl, th, sh) : tl;
+        uint32_t oh = rot ? __builtin_amdgcn_alignbit(th, tl, sh) : th;
+        uint32_t bl = gshfl(ol, src), bh = gshfl(oh, src);
+        uint32_t b1l = gshfl(bl, n1), b1h = gshfl(bh, n1), b2l = gshfl(bl, n2), b2h = gshfl(bh, n2);
+        lo = kchi(bl, b1l, b2l);
+        hi = kchi(bh, b1h, b2h);
+        if (i == 0) {
+            lo ^= (uint32_t)KECCAK_RC[round];
+            hi ^= (uint32_t)(KECCAK_RC[round] >> 32);
+        }
+    }
+}
+
+// Keccak-256 of len bytes at m (8-byte aligned; LDS or global) by a 32-lane group (gl = lane in
+// group); every lane of the group returns the digest words.
+GSV_DI void keccak256_coop(uint32_t h[8], const uint8_t* m, uint32_t len, int gl) {
+    const int i = gl < 25 ? gl : 24;
+    uint32_t lo = 0, hi = 0;
+    const uint64_t* q = (const uint64_t*)m;
+    uint32_t nb = len / 136 + 1;
+    for (uint32_t b = 0; b < nb; b++) {
+        if (gl < 17) {
+            uint64_t w;
+            if (b + 1 < nb) {
+                w = q[17 * b + gl];
+            } else {
+                int32_t avail = (int32_t)(len - 136 * b) - 8 * gl;
+                w = avail >= 8 ? q[17 * b + gl] : avail > 0 ? q[17 * b + gl] & ((1ull << (8 * avail)) - 1ull) : 0ull;
+                uint32_t rem = len - 136 * b;
+                if ((rem >> 3) == (uint32_t)gl) w ^= 0x01ull << (8 * (rem & 7u));
+                if (gl == 16) w ^= 0x8000000000000000ULL;
+            }
+            lo ^= (uint32_t)w;
+            hi ^= (uint32_t)(w >> 32);
+        }
+        keccakf_coop(lo, hi, i);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        h[2 * k] = gshfl(lo, k);
+        h[2 * k + 1] = gshfl(hi, k);
+    }
+}
+
 // Keccak-256 of the 64-byte string X||Y given as big-endian 256-bit limb arrays
 // (address derivation: crypto.Keccak256(pub[1:]) in core/types/transaction_signing.go:244).
 GSV_DI void keccak256_xy(uint32_t h[8], const uint32_t x[8], const uint32_t y[8]) {
