@@ -53,6 +53,18 @@ HBM_PEAK_GBPS = 8000.0
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "latest", "pmc_summary.json")
 
 
+def pmc_valu_issue(kernel: str):
+    """VALU instructions issued per SIMD cycle for `kernel` from the committed SQ counter pass
+    (SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), tools/pmc_summary.py).  A wave64 VALU
+    instruction occupies a SIMD16 for >= 4 cycles, so 0.25 means the SIMDs issue VALU work every
+    cycle they can.  None when no summary is committed."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            return float(json.load(f)[kernel]["valu_issue_per_simd_cycle"])
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this bench
     (tools/profile_round.sh -> tools/pmc_summary.py): FETCH_SIZE x 2 (gfx950 correction,
@@ -474,6 +486,7 @@ def main():
                          # by design: one 80-byte affine comb entry per 16-bit window of u1 (16 per
                          # recovery) from the 80 MiB Infinity-Cache-resident table
                          "comb_table_bytes_per_launch": N_SIGS * 16 * 80,
+                         "valu_issue_per_simd_cycle": pmc_valu_issue("gsv::k_ecrecover"),
                          "kernel": "k_ecrecover", "kernel_avg_ms": round(k_avg_ms, 4),
                          "algorithmic_per_unit": f"{MACS_PER_RECOVERY} 32x32-bit partial products per recovery"},
             "cpu_baseline": cpu,
