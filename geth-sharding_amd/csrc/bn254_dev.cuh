@@ -314,9 +314,10 @@ GSV_DI void fp6_frob_p2(fp6& e, const fp6& a) {
     fp2_mul_fp(e.y, a.y, k);
     e.z = a.z;
 }
-// gfp6.go:96-123 (Karatsuba)
-static BN_NI void fp6_mul_p(fp6* e, const fp6* pa, const fp6* pb) {
-    const fp6 a = *pa, b = *pb;
+// gfp6.go:96-123 (Karatsuba).  The *_i forms are always inlined (the Miller loop keeps its whole
+// state in VGPRs); the *_p forms are out-of-line wrappers for the colder callers.
+GSV_DI void fp6_mul_i(fp6& e, const fp6& pa_, const fp6& pb_) {
+    const fp6 a = pa_, b = pb_;
     fp2 v0, v1, v2, t0, t1, tz, ty, tx;
     fp2_mul(v0, a.z, b.z);
     fp2_mul(v1, a.y, b.y);
@@ -341,16 +342,17 @@ static BN_NI void fp6_mul_p(fp6* e, const fp6* pa, const fp6* pb) {
     fp2_sub(tx, tx, v0);
     fp2_add(tx, tx, v1);
     fp2_sub(tx, tx, v2);
-    e->x = tx;
-    e->y = ty;
-    e->z = tz;
+    e.x = tx;
+    e.y = ty;
+    e.z = tz;
 }
+static BN_NI void fp6_mul_p(fp6* e, const fp6* pa, const fp6* pb) { fp6_mul_i(*e, *pa, *pb); }
 GSV_DI void fp6_mul(fp6& e, const fp6& a, const fp6& b) { fp6_mul_p(&e, &a, &b); }
 // e = a * (by tau + bz) (a line's sparse factor, x coefficient 0): 5 F_p^2 products instead of 6;
 // the same field element as fp6_mul with b.x = 0, hence the same canonical words.
-static BN_NI void fp6_mul_sparse_p(fp6* e, const fp6* pa, const fp2* pby, const fp2* pbz) {
-    const fp6 a = *pa;
-    const fp2 by = *pby, bz = *pbz;
+GSV_DI void fp6_mul_sparse_i(fp6& e, const fp6& pa_, const fp2& pby_, const fp2& pbz_) {
+    const fp6 a = pa_;
+    const fp2 by = pby_, bz = pbz_;
     fp2 v0, v1, t0, t1, tx, ty, tz;
     fp2_mul(v0, a.z, bz);
     fp2_mul(v1, a.y, by);
@@ -364,15 +366,21 @@ static BN_NI void fp6_mul_sparse_p(fp6* e, const fp6* pa, const fp2* pby, const 
     fp2_sub(ty, ty, v1);
     fp2_mul(tx, a.x, bz);
     fp2_add(tx, tx, v1);
-    e->x = tx;
-    e->y = ty;
-    e->z = tz;
+    e.x = tx;
+    e.y = ty;
+    e.z = tz;
 }
-static BN_NI void fp6_mul_fp2_p(fp6* e, const fp6* a, const fp2* b) {
-    fp2_mul(e->x, a->x, *b);
-    fp2_mul(e->y, a->y, *b);
-    fp2_mul(e->z, a->z, *b);
+static BN_NI void fp6_mul_sparse_p(fp6* e, const fp6* pa, const fp2* pby, const fp2* pbz) {
+    fp6_mul_sparse_i(*e, *pa, *pby, *pbz);
 }
+GSV_DI void fp6_mul_fp2_i(fp6& e, const fp6& a_, const fp2& b_) {
+    const fp6 a = a_;
+    const fp2 b = b_;
+    fp2_mul(e.x, a.x, b);
+    fp2_mul(e.y, a.y, b);
+    fp2_mul(e.z, a.z, b);
+}
+static BN_NI void fp6_mul_fp2_p(fp6* e, const fp6* a, const fp2* b) { fp6_mul_fp2_i(*e, *a, *b); }
 GSV_DI void fp6_mul_fp2(fp6& e, const fp6& a, const fp2& b) { fp6_mul_fp2_p(&e, &a, &b); }
 GSV_DI void fp6_mul_fp(fp6& e, const fp6& a, const fp& b) { fp2_mul_fp(e.x, a.x, b); fp2_mul_fp(e.y, a.y, b); fp2_mul_fp(e.z, a.z, b); }
 // gfp6.go:140-149: tau (x tau^2 + y tau + z) = y tau^2 + z tau + x xi

@@ -68,21 +68,22 @@ static BN_NI void fp12_mul_p(fp12* pe, const fp12* pa, const fp12* pb) {
 }
 GSV_DI void fp12_mul(fp12& e, const fp12& a, const fp12& b) { fp12_mul_p(&e, &a, &b); }
 // gfp12.go:129-143
-static BN_NI void fp12_sqr_p(fp12* pe, const fp12* pa) {
-    const fp12 a = *pa;
-    fp12& e = *pe;
+// (the _i form is always inlined: the Miller loop's accumulator never leaves VGPRs)
+GSV_DI void fp12_sqr_i(fp12& e, const fp12& a_) {
+    const fp12 a = a_;
     fp6 v0, t, ty;
-    fp6_mul(v0, a.x, a.y);
+    fp6_mul_i(v0, a.x, a.y);
     fp6_mul_tau(t, a.x);
     fp6_add(t, a.y, t);
     fp6_add(ty, a.x, a.y);
-    fp6_mul(ty, ty, t);
+    fp6_mul_i(ty, ty, t);
     fp6_sub(ty, ty, v0);
     fp6_mul_tau(t, v0);
     fp6_sub(ty, ty, t);
     fp6_add(e.x, v0, v0);
     e.y = ty;
 }
+static BN_NI void fp12_sqr_p(fp12* pe, const fp12* pa) { fp12_sqr_i(*pe, *pa); }
 GSV_DI void fp12_sqr(fp12& e, const fp12& a) { fp12_sqr_p(&e, &a); }
 // Squaring in the cyclotomic subgroup (Granger-Scott, "Faster squaring in the cyclotomic subgroup of
 // sixth degree extensions", PKC 2010): 9 F_p^2 squarings instead of two F_p^6 products.  Valid for
@@ -90,9 +91,8 @@ GSV_DI void fp12_sqr(fp12& e, const fp12& a) { fp12_sqr_p(&e, &a); }
 // (optate.go:218-222) — and it yields the same field element (hence the same canonical words) as
 // fp12_sqr there.  Coefficients of a = sum c_k w^k over F_p^2 (w^2 = tau, tau^3 = xi):
 // c0 = y.z, c1 = x.z, c2 = y.y, c3 = x.y, c4 = y.x, c5 = x.x.
-static BN_NI void fp12_cyclo_sqr_p(fp12* pe, const fp12* pa) {
-    const fp12 a = *pa;
-    fp12& e = *pe;
+GSV_DI void fp12_cyclo_sqr_i(fp12& e, const fp12& pa_) {
+    const fp12 a = pa_;
     const fp2 &x0 = a.y.z, &x1 = a.y.y, &x2 = a.y.x, &x3 = a.x.z, &x4 = a.x.y, &x5 = a.x.x;
     fp2 t0, t1, t2, t3, t4, t5, t6, t7, t8, u;
     fp2_sqr(t0, x4);
@@ -141,6 +141,7 @@ static BN_NI void fp12_cyclo_sqr_p(fp12* pe, const fp12* pa) {
     fp2_add(u, u, u);
     fp2_add(e.x.x, u, t7);
 }
+static BN_NI void fp12_cyclo_sqr_p(fp12* pe, const fp12* pa) { fp12_cyclo_sqr_i(*pe, *pa); }
 GSV_DI void fp12_cyclo_sqr(fp12& e, const fp12& a) { fp12_cyclo_sqr_p(&e, &a); }
 // gfp12.go:145-160
 GSV_DI void fp12_inv(fp12& e, const fp12& a) {
@@ -155,24 +156,33 @@ GSV_DI void fp12_inv(fp12& e, const fp12& a) {
     fp6_mul(e.x, nx, t2);
     fp6_mul(e.y, a.y, t2);
 }
-// gfp12.go:113-127 with power = u (63 bits, top bit set); only called on cyclotomic-subgroup elements
+// NAF of u: u = U_NAF_POS - U_NAF_NEG, digit 62 = +1 (also used by the G2 subgroup predicate)
+constexpr uint64_t U_NAF_POS = 0x450a14044a890a01ULL;
+constexpr uint64_t U_NAF_NEG = 0x0020815000200010ULL;
+// gfp12.go:113-127 with power = u; only called on cyclotomic-subgroup elements (the final
+// exponentiation's hard part), where a^-1 = conj(a): the NAF of u needs 23 products instead of the
+// 27 of its binary expansion, and the result is the same field element a^u (same canonical words).
+// (Inlining this loop down to the F_p product was measured slower: 14.6 -> 17.9 ms per 65,536
+// final exponentiations, heavy spills of the 96-word operands.)
 static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
-    fp12 sum = *a;  // the leading bit: 1^2 * a
+    fp12 sum = *a;  // the leading digit: 1^2 * a
 #pragma unroll 1
     for (int i = 61; i >= 0; i--) {
-        fp12 t;
-        fp12_cyclo_sqr(t, sum);  // a is in the cyclotomic subgroup (final exponentiation hard part)
-        if ((BN_U >> i) & 1) fp12_mul(sum, t, *a);
-        else sum = t;
+        fp12_cyclo_sqr(sum, sum);
+        bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
+        if (pos || neg) {
+            fp12 t = *a;
+            if (neg) fp6_neg(t.x, t.x);
+            fp12_mul(sum, sum, t);
+        }
     }
     *c = sum;
 }
 
 // ---------------------------------------------------------------- twist points (twist.go)
 // twist.go:136-162 dbl-2009-l (t is not updated, as in the reference)
-static BN_NI void g2_double_p(g2j* pc, const g2j* pa) {
-    const g2j a = *pa;
-    g2j& c = *pc;
+GSV_DI void g2_double_i(g2j& c, const g2j& pa_) {
+    const g2j a = pa_;
     fp2 A, B, C, t, t2, d, e, f;
     fp2_sqr(A, a.x);
     fp2_sqr(B, a.y);
@@ -199,6 +209,7 @@ static BN_NI void g2_double_p(g2j* pc, const g2j* pa) {
     r.t = a.t;
     c = r;
 }
+static BN_NI void g2_double_p(g2j* pc, const g2j* pa) { g2_double_i(*pc, *pa); }
 GSV_DI void g2_double(g2j& c, const g2j& a) { g2_double_p(&c, &a); }
 // twist.go:73-134 add-2007-bl with its infinity / doubling cases
 static BN_NI void g2_add_p(g2j* pc, const g2j* pa, const g2j* pb) {
@@ -246,10 +257,9 @@ static BN_NI void g2_add_p(g2j* pc, const g2j* pa, const g2j* pb) {
 GSV_DI void g2_add(g2j& c, const g2j& a, const g2j& b) { g2_add_p(&c, &a, &b); }
 // c = a + q with q affine (z = 1): madd-2007-bl, 8M + 3S instead of the general 11M + 5S.  Used only
 // inside the subgroup predicate, whose boolean outcome does not depend on the formulas chosen.
-static BN_NI void g2_add_mixed_p(g2j* pc, const g2j* pa, const g2a* pq) {
-    const g2j a = *pa;
-    const g2a q = *pq;
-    g2j& c = *pc;
+GSV_DI void g2_add_mixed_i(g2j& c, const g2j& pa_, const g2a& pq_) {
+    const g2j a = pa_;
+    const g2a q = pq_;
     if (fp2_is_zero(a.z)) {
         c.x = q.x;
         c.y = q.y;
@@ -264,7 +274,7 @@ static BN_NI void g2_add_mixed_p(g2j* pc, const g2j* pa, const g2a* pq) {
     fp2_mul(s2, q.y, t);
     fp2_sub(h, u2, a.x);
     fp2_sub(t, s2, a.y);
-    if (fp2_is_zero(h) && fp2_is_zero(t)) {
+    if (fp2_is_zero(h) && fp2_is_zero(t)) {  // out of line: never taken on the hot path
         g2_double(c, a);
         return;
     }
@@ -288,6 +298,7 @@ static BN_NI void g2_add_mixed_p(g2j* pc, const g2j* pa, const g2a* pq) {
     o.t = a.t;
     c = o;
 }
+static BN_NI void g2_add_mixed_p(g2j* pc, const g2j* pa, const g2a* pq) { g2_add_mixed_i(*pc, *pa, *pq); }
 // psi(X : Y : Z) = (conj(X) xi^((p-1)/3) : conj(Y) xi^((p-1)/2) : conj(Z)) — the p-power
 // Frobenius carried through the twist isomorphism (optate.go:173-176 applies it to affine Q)
 GSV_DI void g2_psi(g2j& o, const g2j& a) {
@@ -302,10 +313,7 @@ GSV_DI void g2_psi(g2j& o, const g2j& a) {
     o.t = a.t;
 }
 // twist.go:47-63: y^2 == x^3 + 3/xi and Q in the order-r subgroup
-// NAF of u: u = U_NAF_POS - U_NAF_NEG, digit 62 = +1
-constexpr uint64_t U_NAF_POS = 0x450a14044a890a01ULL;
-constexpr uint64_t U_NAF_NEG = 0x0020815000200010ULL;
-static BN_NI bool g2_in_subgroup(const g2a* q) {
+GSV_DI bool g2_in_subgroup(const g2a* q) {
     fp2 y2, x3, b;
     fp2_sqr(y2, q->y);
     fp2_sqr(x3, q->x);
@@ -331,13 +339,12 @@ static BN_NI bool g2_in_subgroup(const g2a* q) {
     mq.x = q->x;
     fp2_neg(mq.y, q->y);
     g2j uq = a;  // leading digit +1 at bit 62
+    // inlined down to the F_p product: the running point stays in VGPRs
 #pragma unroll 1
     for (int i = 61; i >= 0; i--) {
-        g2j t;
-        g2_double(t, uq);
-        if ((U_NAF_POS >> i) & 1) g2_add_mixed_p(&uq, &t, q);
-        else if ((U_NAF_NEG >> i) & 1) g2_add_mixed_p(&uq, &t, &mq);
-        else uq = t;
+        g2_double_i(uq, uq);
+        bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
+        if (pos || neg) g2_add_mixed_i(uq, uq, neg ? mq : *q);
     }
     g2j lhs, p1, p2, rhs, tmp;
     g2_add(lhs, uq, a);          // [u+1]Q
@@ -356,14 +363,10 @@ static BN_NI bool g2_in_subgroup(const g2a* q) {
 
 // ---------------------------------------------------------------- Miller loop (optate.go)
 // optate.go:3-50 (mixed addition r + p, p affine with t = 1; r2 = p.y^2)
-static BN_NI void line_add_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g2a* pp, const g1a* pq, const fp2* pr2) {
-    fp2& a = *pa;
-    fp2& b = *pb;
-    fp2& c = *pc;
-    g2j& r = *pr;
-    const g2a p = *pp;
-    const g1a q = *pq;
-    const fp2 r2 = *pr2;
+GSV_DI void line_add_i(fp2& a, fp2& b, fp2& c, g2j& r, const g2a& pp, const g1a& pq, const fp2& pr2) {
+    const g2a p = pp;
+    const g1a q = pq;
+    const fp2 r2 = pr2;
     fp2 B, D, H, I, E, J, L1, V, t, t2;
     fp2_mul(B, p.x, r.t);
     fp2_add(D, p.y, r.z);
@@ -408,16 +411,15 @@ static BN_NI void line_add_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g2a* pp, 
     fp2_add(b, b, b);
     r = o;
 }
+static BN_NI void line_add_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g2a* pp, const g1a* pq, const fp2* pr2) {
+    line_add_i(*pa, *pb, *pc, *pr, *pp, *pq, *pr2);
+}
 GSV_DI void line_add(fp2& a, fp2& b, fp2& c, g2j& r, const g2a& p, const g1a& q, const fp2& r2) {
     line_add_p(&a, &b, &c, &r, &p, &q, &r2);
 }
 // optate.go:52-92
-static BN_NI void line_double_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g1a* pq) {
-    fp2& a = *pa;
-    fp2& b = *pb;
-    fp2& c = *pc;
-    g2j& r = *pr;
-    const g1a q = *pq;
+GSV_DI void line_double_i(fp2& a, fp2& b, fp2& c, g2j& r, const g1a& pq) {
+    const g1a q = pq;
     fp2 A, B, C, D, E, G, t;
     fp2_sqr(A, r.x);
     fp2_sqr(B, r.y);
@@ -460,22 +462,26 @@ static BN_NI void line_double_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g1a* p
     fp2_mul_fp(c, c, q.y);
     r = o;
 }
+static BN_NI void line_double_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g1a* pq) {
+    line_double_i(*pa, *pb, *pc, *pr, *pq);
+}
 GSV_DI void line_double(fp2& a, fp2& b, fp2& c, g2j& r, const g1a& q) { line_double_p(&a, &b, &c, &r, &q); }
 // optate.go:94-112
-static BN_NI void mul_line(fp12* ret, const fp2* a, const fp2* b, const fp2* c) {
-    fp6 a2, t3, rx;
+GSV_DI void mul_line_i(fp12& ret, const fp2& a, const fp2& b, const fp2& c) {
+    // ordered so that at most ret + one F_p^6 temporary + the line are live at a time
+    fp6 s, a2;
     fp2 bc;
-    fp6_mul_sparse_p(&a2, &ret->x, a, b);  // (0, a, b) * ret.x
-    fp6_mul_fp2(t3, ret->y, *c);
-    fp2_add(bc, *b, *c);
-    fp6_add(rx, ret->x, ret->y);
-    fp6_mul_sparse_p(&rx, &rx, a, &bc);  // * (0, a, b + c)
-    fp6_sub(rx, rx, a2);
-    fp6_sub(rx, rx, t3);
-    ret->x = rx;
+    fp6_add(s, ret.x, ret.y);
+    fp6_mul_sparse_i(a2, ret.x, a, b);  // (0, a, b) * ret.x
+    fp6_mul_fp2_i(ret.y, ret.y, c);      // t3
+    fp2_add(bc, b, c);
+    fp6_mul_sparse_i(s, s, a, bc);       // * (0, a, b + c)
+    fp6_sub(s, s, a2);
+    fp6_sub(ret.x, s, ret.y);
     fp6_mul_tau(a2, a2);
-    fp6_add(ret->y, t3, a2);
+    fp6_add(ret.y, ret.y, a2);
 }
+static BN_NI void mul_line(fp12* ret, const fp2* a, const fp2* b, const fp2* c) { mul_line_i(*ret, *a, *b, *c); }
 
 // optate.go:122-210 for affine q (twist) and p (G1), neither at infinity
 GSV_DI void miller(fp12& ret, const g2a& A, const g1a& B) {
@@ -531,12 +537,12 @@ static BN_NI void final_exp(fp12* out, const fp12* in) {
     fp12_mul(t1, t1, t2);
     fp12_frob_p2(t2, t1);
     fp12_mul(t1, t1, t2);
-    fp12_frob(fp1, t1);
-    fp12_frob_p2(fp2_, t1);
-    fp12_frob(fp3, fp2_);
     fp12_exp_u(&fu, &t1);
     fp12_exp_u(&fu2, &fu);
     fp12_exp_u(&fu3, &fu2);
+    fp12_frob(fp1, t1);
+    fp12_frob_p2(fp2_, t1);
+    fp12_frob(fp3, fp2_);
     fp12_frob(y3, fu);
     fp12 fu2p, fu3p;
     fp12_frob(fu2p, fu2);
@@ -680,15 +686,18 @@ GSV_DI void pts_load(g1a& P, g2a& Q, const uint32_t* __restrict__ pts, uint32_t 
     soa_load(Q.y.y, pts, n, j, 5);
 }
 
-__global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ check_first, uint32_t nchecks,
+// A lane runs the loop over a group of <= k of its check's pairs (k = 4 covers a whole 4-pair check;
+// smaller k when the batch is too small to give every SIMD work — the host's choice), and k_bn_final
+// multiplies a check's lane values: the same exact product, so the same verdict.
+__global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ lane_first, uint32_t nlanes,
                                                   const uint32_t* __restrict__ pidx, const uint8_t* __restrict__ pstat,
                                                   const uint32_t* __restrict__ pts, uint32_t npairs,
                                                   uint32_t* __restrict__ rs /* [64 words][npairs] */,
                                                   uint8_t* __restrict__ cstat,
-                                                  uint32_t* __restrict__ fv /* [96 words][nchecks] */) {
+                                                  uint32_t* __restrict__ fv /* [96 words][nlanes] */) {
     uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchecks) return;
-    uint32_t b = check_first[c], e = check_first[c + 1];
+    if (c >= nlanes) return;
+    uint32_t b = lane_first[c], e = lane_first[c + 1];
     bool bad = false, any = false;
     for (uint32_t q = b; q < e; q++) {
         uint32_t j = pidx[q];
@@ -711,11 +720,15 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ c
     fp12 f;
     fp12_one(f);
     fp2 la, lb, lc;
+    // The loop body is inlined down to the out-of-line F_p product (whose 28 VGPRs are all it
+    // clobbers), so f, R and the line stay in registers: no per-lane scratch on the hot path.  A
+    // pair's doubling step and (on NAF digits) its addition step share one inlined mul_line.
 #pragma unroll 1
     for (int i = 64; i > 0; i--) {
-        if (i != 64) fp12_sqr(f, f);
+        if (i != 64) fp12_sqr_i(f, f);
         uint64_t bit = 1ull << (i - 1);
         bool add = ((NAF_POS | NAF_NEG) & bit) != 0;
+#pragma unroll 1
         for (uint32_t q = b; q < e; q++) {
             uint32_t j = pidx[q];
             if (pstat[j] != PS_OK) continue;
@@ -724,19 +737,22 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ c
             soa_load(P.y, pts, npairs, j, 1);
             g2j r;
             g2j_load(r, rs, npairs, j);
-            line_double(la, lb, lc, r, P);
-            mul_line(&f, &la, &lb, &lc);
-            if (add) {  // Q is only needed on the NAF's nonzero digits
-                g2a Q;
-                soa_load(Q.x.x, pts, npairs, j, 2);
-                soa_load(Q.x.y, pts, npairs, j, 3);
-                soa_load(Q.y.x, pts, npairs, j, 4);
-                soa_load(Q.y.y, pts, npairs, j, 5);
-                fp2 r2;
-                fp2_sqr(r2, Q.y);
-                if (NAF_NEG & bit) fp2_neg(Q.y, Q.y);
-                line_add(la, lb, lc, r, Q, P, r2);
-                mul_line(&f, &la, &lb, &lc);
+#pragma unroll 1
+            for (int k = 0; k < (add ? 2 : 1); k++) {
+                if (k == 0) {
+                    line_double_i(la, lb, lc, r, P);
+                } else {  // Q is only needed on the NAF's nonzero digits
+                    g2a Q;
+                    soa_load(Q.x.x, pts, npairs, j, 2);
+                    soa_load(Q.x.y, pts, npairs, j, 3);
+                    soa_load(Q.y.x, pts, npairs, j, 4);
+                    soa_load(Q.y.y, pts, npairs, j, 5);
+                    fp2 r2;
+                    fp2_sqr(r2, Q.y);
+                    if (NAF_NEG & bit) fp2_neg(Q.y, Q.y);
+                    line_add_i(la, lb, lc, r, Q, P, r2);
+                }
+                mul_line_i(f, la, lb, lc);
             }
             g2j_store(rs, npairs, j, r);
         }
@@ -769,21 +785,36 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ c
         line_add(la, lb, lc, r, mq2, P, r2);
         mul_line(&f, &la, &lb, &lc);
     }
-    fp12_store(fv, nchecks, c, f);
+    fp12_store(fv, nlanes, c, f);
 }
 
-__global__ __launch_bounds__(64) void k_bn_final(uint32_t nchecks, const uint8_t* __restrict__ cstat,
-                                                 const uint32_t* __restrict__ fv, uint8_t* __restrict__ verdict) {
+__global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
+                                                 const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv,
+                                                 uint32_t nlanes, uint8_t* __restrict__ verdict) {
     uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchecks) return;
-    uint8_t cs = cstat[c];
-    if (cs == CS_BAD) {
+    uint32_t l0 = check_lane[c], l1 = check_lane[c + 1];
+    bool bad = false;
+    for (uint32_t l = l0; l < l1; l++) bad = bad || lstat[l] == CS_BAD;
+    if (bad) {
         verdict[c] = GSV_PAIRING_BAD_INPUT;
         return;
     }
+    // product of the check's lane values; finalExponentiation(1) == 1 when no pair is finite
     fp12 acc;
-    if (cs == CS_ONE) fp12_one(acc);  // finalExponentiation(1) == 1 (all pairs at infinity / no pairs)
-    else fp12_load(acc, fv, nchecks, c);
+    bool any = false;
+    for (uint32_t l = l0; l < l1; l++) {
+        if (lstat[l] != CS_OK) continue;
+        if (!any) {
+            fp12_load(acc, fv, nlanes, l);
+            any = true;
+        } else {
+            fp12 t;
+            fp12_load(t, fv, nlanes, l);
+            fp12_mul(acc, acc, t);
+        }
+    }
+    if (!any) fp12_one(acc);
     fp12 r;
     final_exp(&r, &acc);
     verdict[c] = fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
@@ -1010,10 +1041,10 @@ hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, u
 }
 
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
-                                const uint32_t* d_check_first, const uint32_t* d_pidx, uint32_t nchecks,
-                                uint8_t* d_pstat, uint32_t* d_pts, uint32_t* d_rs, uint8_t* d_cstat, uint32_t* d_fv,
-                                uint8_t* d_verdict, hipStream_t st, void (*timer_begin)(void*, int),
-                                void (*timer_end)(void*, int), void* tctx) {
+                                const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
+                                const uint32_t* d_check_lane, uint32_t nchecks, uint8_t* d_pstat, uint32_t* d_pts,
+                                uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv, uint8_t* d_verdict, hipStream_t st,
+                                void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx) {
     if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
         hipLaunchKernelGGL(bn::k_bn_prepare, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
@@ -1024,14 +1055,14 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
     }
     if (nchecks) {
         if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
-        hipLaunchKernelGGL(bn::k_bn_miller, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_first, nchecks,
-                           d_pidx, d_pstat, d_pts, npairs, d_rs, d_cstat, d_fv);
+        hipLaunchKernelGGL(bn::k_bn_miller, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
+                           d_pidx, d_pstat, d_pts, npairs, d_rs, d_lstat, d_fv);
         if (timer_end) timer_end(tctx, GSV_K_PAIRING);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
-        hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, nchecks, d_cstat, d_fv,
-                           d_verdict);
+        hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_lane, nchecks,
+                           d_lstat, d_fv, nlanes, d_verdict);
         if (timer_end) timer_end(tctx, GSV_K_BN_FINAL);
     }
     return hipGetLastError();

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -643,9 +644,26 @@ struct BnTables {
     std::vector<uint64_t> pair_src;     // slot-major pair order
     std::vector<uint32_t> check_first;  // check c's pairs: pidx[check_first[c] .. check_first[c+1])
     std::vector<uint32_t> pidx;         // check-major position -> slot-major pair index
+    std::vector<uint32_t> lane_first;   // Miller lane l's pairs: pidx[lane_first[l] .. lane_first[l+1])
+    std::vector<uint32_t> check_lane;   // check c's Miller lanes: [check_lane[c], check_lane[c+1])
     std::vector<uint8_t> bad_len;
 };
-static int bn_tables(const uint64_t* off, size_t n, uint64_t base, BnTables& t) {
+// Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
+// lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
+// and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
+// batches split a check over more lanes (k = 2, 1).  GSV_BN_PAIRS_PER_LANE forces k (A/B timing).
+static uint32_t bn_pairs_per_lane(size_t np, int cus) {
+    if (const char* e = getenv("GSV_BN_PAIRS_PER_LANE")) {
+        int k = atoi(e);
+        if (k >= 1) return (uint32_t)k;
+    }
+    const size_t waves = 1;
+    size_t target = (size_t)std::max(cus, 1) * 4 * 64 * waves;
+    for (uint32_t k = 4; k > 1; k >>= 1)
+        if ((np + k - 1) / k >= target) return k;
+    return 1;
+}
+static int bn_tables(const uint64_t* off, size_t n, uint64_t base, int cus, BnTables& t) {
     t.check_first.resize(n + 1);
     t.bad_len.assign(n, 0);
     size_t np = 0, maxk = 0;
@@ -693,33 +711,53 @@ static int bn_tables(const uint64_t* off, size_t n, uint64_t base, BnTables& t) 
         }
     }
     t.check_first[n] = (uint32_t)q;
+    uint32_t k = bn_pairs_per_lane(np, cus);
+    t.check_lane.resize(n + 1);
+    t.lane_first.clear();
+    t.lane_first.reserve(n + np / k + 2);
+    for (size_t c = 0; c < n; c++) {
+        t.check_lane[c] = (uint32_t)t.lane_first.size();
+        uint32_t b = t.check_first[c], e = t.check_first[c + 1];
+        t.lane_first.push_back(b);  // a check without pairs still gets one (empty) lane
+        for (uint32_t p = b + k; p < e; p += k) t.lane_first.push_back(p);
+    }
+    t.check_lane[n] = (uint32_t)t.lane_first.size();
+    t.lane_first.push_back((uint32_t)q);
     return GSV_SUCCESS;
+}
+static int device_cus(int device) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
+    return cus;
 }
 
 // enqueue the three pairing kernels; d_in already in HBM, tables from the host
 static int bn_run(gsv_ctx* c, const uint8_t* d_in, const BnTables& t, size_t n, uint8_t* d_verdict,
                   hipStream_t st) {
     size_t np = t.pair_src.size();
-    size_t need = al(np * 8 + 8) + al((n + 1) * 4) + al(np * 4 + 4) + al(np + 1) + al(np * 48 * 4 + 4) +
-                  al(np * 64 * 4 + 4) + al(n + 1) + al(n * 96 * 4 + 4);
+    size_t nl = t.lane_first.size() - 1;
+    size_t need = al(np * 8 + 8) + al((nl + 1) * 4) + al((n + 1) * 4) + al(np * 4 + 4) + al(np + 1) +
+                  al(np * 48 * 4 + 4) + al(np * 64 * 4 + 4) + al(nl + 1) + al(nl * 96 * 4 + 4);
     work_begin(c, st);
     int rc = work_reserve(c, need + 4096);
     if (rc) return rc;
     Carve cv(c->work);
     uint64_t* d_src = cv.take<uint64_t>(np * 8 + 8);
-    uint32_t* d_first = cv.take<uint32_t>((n + 1) * 4);
+    uint32_t* d_lfirst = cv.take<uint32_t>((nl + 1) * 4);
+    uint32_t* d_clane = cv.take<uint32_t>((n + 1) * 4);
     uint32_t* d_pidx = cv.take<uint32_t>(np * 4 + 4);
     uint8_t* d_pstat = cv.take<uint8_t>(np + 1);
     uint32_t* d_pts = cv.take<uint32_t>(np * 48 * 4 + 4);
     uint32_t* d_rs = cv.take<uint32_t>(np * 64 * 4 + 4);
-    uint8_t* d_cstat = cv.take<uint8_t>(n + 1);
-    uint32_t* d_fv = cv.take<uint32_t>(n * 96 * 4 + 4);
+    uint8_t* d_lstat = cv.take<uint8_t>(nl + 1);
+    uint32_t* d_fv = cv.take<uint32_t>(nl * 96 * 4 + 4);
     if (np) HIPCHK(hipMemcpyAsync(d_src, t.pair_src.data(), np * 8, hipMemcpyHostToDevice, st));
     if (np) HIPCHK(hipMemcpyAsync(d_pidx, t.pidx.data(), np * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_first, t.check_first.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_lfirst, t.lane_first.data(), (nl + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_clane, t.check_lane.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
     c->cur_stream = st;
-    HIPCHK(gsv::launch_bn256_pairing(d_in, d_src, (uint32_t)np, d_first, d_pidx, (uint32_t)n, d_pstat, d_pts, d_rs,
-                                     d_cstat, d_fv, d_verdict, st, hook_begin, hook_end, c));
+    HIPCHK(gsv::launch_bn256_pairing(d_in, d_src, (uint32_t)np, d_lfirst, d_pidx, (uint32_t)nl, d_clane, (uint32_t)n,
+                                     d_pstat, d_pts, d_rs, d_lstat, d_fv, d_verdict, st, hook_begin, hook_end, c));
     // errBadPairingInput for ragged lengths overrides the kernel's verdict (those checks had no pairs)
     static const uint8_t bad = GSV_PAIRING_BAD_INPUT;
     for (size_t i = 0; i < n; i++)
@@ -734,7 +772,7 @@ int gsv_bn256_pairing_check_batch_dev(gsv_ctx* c, const uint8_t* d_in, const uin
     if (n == 0) return GSV_SUCCESS;
     if (n > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
     BnTables t;
-    int rc = bn_tables(h_off, n, 0, t);
+    int rc = bn_tables(h_off, n, 0, device_cus(c->device), t);
     if (rc) return rc;
     if (!t.pair_src.empty() && !d_in) return GSV_E_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->wmu);
@@ -747,7 +785,7 @@ int gsv_bn256_pairing_check_batch(gsv_ctx* c, const uint8_t* in, const uint64_t*
     if (n == 0) return GSV_SUCCESS;
     if (n > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
     BnTables t;
-    int rc = bn_tables(off, n, off[0], t);
+    int rc = bn_tables(off, n, off[0], device_cus(c->device), t);
     if (rc) return rc;
     if (!t.pair_src.empty() && !in) return GSV_E_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);

@@ -40,8 +40,8 @@ def test_pairing_each_vector_alone(ctx):
         assert out[0] == r["verdict"], r.get("name", r.get("note"))
 
 
-def test_pairing_random_batch_vs_oracle(ctx, oracle):
-    rng = random.Random(17)
+def _random_inputs(oracle, seed):
+    rng = random.Random(seed)
     g1 = [oracle.bn256_g1_mul(rng.randrange(1, R)) for _ in range(12)]
     g2 = [oracle.bn256_g2_mul(rng.randrange(1, R)) for _ in range(6)]
     inputs = []
@@ -67,10 +67,27 @@ def test_pairing_random_batch_vs_oracle(ctx, oracle):
         else:  # ragged byte length
             inp = bytes(rng.getrandbits(8) for _ in range(rng.choice([1, 64, 191, 193, 383])))
         inputs.append(inp)
+    return inputs
+
+
+def test_pairing_random_batch_vs_oracle(ctx, oracle):
+    inputs = _random_inputs(oracle, 17)
     out = ctx.pairing_check_batch(inputs)
     want = np.array([_v(oracle, x) for x in inputs], np.uint8)
     assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
     assert set(want.tolist()) == {0, 1, 2}
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+def test_pairing_miller_lane_split(ctx, oracle, monkeypatch, k):
+    """A check's pairs split over Miller lanes of <= k pairs (the host picks k from the batch size;
+    GSV_BN_PAIRS_PER_LANE forces it): verdicts must not depend on the split, including ragged checks
+    whose last lane is short, lanes holding only infinity pairs, and malformed pairs in any lane."""
+    monkeypatch.setenv("GSV_BN_PAIRS_PER_LANE", str(k))
+    inputs = _random_inputs(oracle, 31 + k)
+    out = ctx.pairing_check_batch(inputs)
+    want = np.array([_v(oracle, x) for x in inputs], np.uint8)
+    assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
 
 
 def test_pairing_empty_batch_and_empty_input(ctx):
