@@ -52,19 +52,23 @@ static BN_NI void fp12_frob_p2_p(fp12* pe, const fp12* pa) {
 }
 GSV_DI void fp12_frob_p2(fp12& e, const fp12& a) { fp12_frob_p2_p(&e, &a); }
 // gfp12.go:94-106
+// Karatsuba over F_p^6: x = (a.x + a.y)(b.x + b.y) - a.x b.x - a.y b.y equals the reference's
+// a.x b.y + b.x a.y, so 3 F_p^6 products instead of 4 give the same canonical words.
 static BN_NI void fp12_mul_p(fp12* pe, const fp12* pa, const fp12* pb) {
     const fp12& a = *pa;
     const fp12& b = *pb;
     fp12& e = *pe;
-    fp6 tx, t, ty;
-    fp6_mul(tx, a.x, b.y);
-    fp6_mul(t, b.x, a.y);
-    fp6_add(tx, tx, t);
-    fp6_mul(ty, a.y, b.y);
-    fp6_mul(t, a.x, b.x);
-    fp6_mul_tau(t, t);
+    fp6 v0, v1, sa, sb, tx;
+    fp6_mul(v0, a.x, b.x);
+    fp6_mul(v1, a.y, b.y);
+    fp6_add(sa, a.x, a.y);
+    fp6_add(sb, b.x, b.y);
+    fp6_mul(tx, sa, sb);
+    fp6_sub(tx, tx, v0);
+    fp6_sub(tx, tx, v1);
+    fp6_mul_tau(v0, v0);
     e.x = tx;
-    fp6_add(e.y, ty, t);
+    fp6_add(e.y, v1, v0);
 }
 GSV_DI void fp12_mul(fp12& e, const fp12& a, const fp12& b) { fp12_mul_p(&e, &a, &b); }
 // gfp12.go:129-143
@@ -174,6 +178,90 @@ static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
             fp12 t = *a;
             if (neg) fp6_neg(t.x, t.x);
             fp12_mul(sum, sum, t);
+        }
+    }
+    *c = sum;
+}
+
+// ---- three-lane cooperative exponentiation by u, for batches too small to give every SIMD a wave.
+// The three lanes of a triple (wave lanes base, base+1, base+2) all hold the whole F_p^12 value;
+// each operation is split into three equal parts selected by the lane's role (same instruction
+// stream, different operands: no divergence), and the parts are exchanged with ds_bpermute.  The
+// dependent chain per exp_u step becomes a third as long; every part computes the same formula as
+// the one-lane routine, so results are the same canonical words.
+GSV_DI uint32_t bperm(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_ds_bpermute(lane << 2, (int)v); }
+template <class T>
+GSV_DI void gather3(T out[3], const T& mine, int base) {  // out[r] = lane (base + r)'s `mine`
+    static_assert(sizeof(T) % 4 == 0, "word-sized");
+    const uint32_t* m = (const uint32_t*)&mine;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        uint32_t* o = (uint32_t*)&out[r];
+#pragma unroll
+        for (int w = 0; w < (int)(sizeof(T) / 4); w++) o[w] = bperm(m[w], base + r);
+    }
+}
+// fp12_cyclo_sqr_i split by coefficient pairs: role 0 squares (x4, x0) and yields c0', c3'; role 1
+// (x2, x3) -> c2', c5'; role 2 (x5, x1) -> c4', c1'
+static BN_NI void fp12_cyclo_sqr3(fp12* pe, const fp12* pa, int role, int base) {
+    const fp12 a = *pa;
+    const fp2 &x0 = a.y.z, &x1 = a.y.y, &x2 = a.y.x, &x3 = a.x.z, &x4 = a.x.y, &x5 = a.x.x;
+    fp2 p = role == 0 ? x4 : role == 1 ? x2 : x5;
+    fp2 q = role == 0 ? x0 : role == 1 ? x3 : x1;
+    fp2 m1 = role == 0 ? x0 : role == 1 ? x1 : x2;
+    fp2 m2 = role == 0 ? x4 : role == 1 ? x5 : x3;
+    fp2 tp, tq, tc, u, sq, tcx;
+    fp2_sqr(tp, p);
+    fp2_sqr(tq, q);
+    fp2_add(u, p, q);
+    fp2_sqr(tc, u);
+    fp2_sub(tc, tc, tp);
+    fp2_sub(tc, tc, tq);  // 2 p q
+    fp2_mul_xi(sq, tp);
+    fp2_add(sq, sq, tq);  // p^2 xi + q^2
+    fp2_mul_xi(tcx, tc);
+    if (role == 2) tc = tcx;  // 2 x5 x1 xi
+    struct { fp2 lo, hi; } mine, all[3];
+    fp2_sub(u, sq, m1);
+    fp2_add(u, u, u);
+    fp2_add(mine.lo, u, sq);  // 3 sq - 2 m1
+    fp2_add(u, tc, m2);
+    fp2_add(u, u, u);
+    fp2_add(mine.hi, u, tc);  // 3 tc + 2 m2
+    gather3(all, mine, base);
+    pe->y.z = all[0].lo;
+    pe->x.y = all[0].hi;
+    pe->y.y = all[1].lo;
+    pe->x.x = all[1].hi;
+    pe->y.x = all[2].lo;
+    pe->x.z = all[2].hi;
+}
+// fp12_mul_p's three F_p^6 products, one per role
+static BN_NI void fp12_mul3(fp12* pe, const fp12* pa, const fp12* pb, int role, int base) {
+    const fp12 a = *pa, b = *pb;
+    fp6 sa, sb, l, r, prod, v[3], tx;
+    fp6_add(sa, a.x, a.y);
+    fp6_add(sb, b.x, b.y);
+    l = role == 0 ? a.x : role == 1 ? a.y : sa;
+    r = role == 0 ? b.x : role == 1 ? b.y : sb;
+    fp6_mul(prod, l, r);
+    gather3(v, prod, base);
+    fp6_sub(tx, v[2], v[0]);
+    fp6_sub(tx, tx, v[1]);
+    fp6_mul_tau(v[0], v[0]);
+    pe->x = tx;
+    fp6_add(pe->y, v[1], v[0]);
+}
+static BN_NI void fp12_exp_u3(fp12* c, const fp12* a, int role, int base) {
+    fp12 sum = *a;
+#pragma unroll 1
+    for (int i = 61; i >= 0; i--) {
+        fp12_cyclo_sqr3(&sum, &sum, role, base);
+        bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
+        if (pos || neg) {
+            fp12 t = *a;
+            if (neg) fp6_neg(t.x, t.x);
+            fp12_mul3(&sum, &sum, &t, role, base);
         }
     }
     *c = sum;
@@ -529,17 +617,28 @@ GSV_DI void miller(fp12& ret, const g2a& A, const g1a& B) {
 }
 
 // optate.go:212-261
-static BN_NI void final_exp(fp12* out, const fp12* in) {
+// base >= 0: the lane is one of the three lanes (base, base+1, base+2) sharing this check (role =
+// its index), which run the three exponentiations by u cooperatively
+static BN_NI void final_exp(fp12* out, const fp12* in, int role, int base) {
+    // every F_p^12 product and cyclotomic squaring goes to the cooperative form on a triple
+#define MUL(e, a, b) (base >= 0 ? fp12_mul3(&(e), &(a), &(b), role, base) : fp12_mul(e, a, b))
+#define CSQR(e, a) (base >= 0 ? fp12_cyclo_sqr3(&(e), &(a), role, base) : fp12_cyclo_sqr(e, a))
     fp12 t1, t2, fp1, fp2_, fp3, fu, fu2, fu3, y0, y1, y2, y3, y4, y5, y6, t0;
     fp6_neg(t1.x, in->x);
     t1.y = in->y;
     fp12_inv(t2, *in);
-    fp12_mul(t1, t1, t2);
+    MUL(t1, t1, t2);
     fp12_frob_p2(t2, t1);
-    fp12_mul(t1, t1, t2);
-    fp12_exp_u(&fu, &t1);
-    fp12_exp_u(&fu2, &fu);
-    fp12_exp_u(&fu3, &fu2);
+    MUL(t1, t1, t2);
+    if (base >= 0) {
+        fp12_exp_u3(&fu, &t1, role, base);
+        fp12_exp_u3(&fu2, &fu, role, base);
+        fp12_exp_u3(&fu3, &fu2, role, base);
+    } else {
+        fp12_exp_u(&fu, &t1);
+        fp12_exp_u(&fu2, &fu);
+        fp12_exp_u(&fu3, &fu2);
+    }
     fp12_frob(fp1, t1);
     fp12_frob_p2(fp2_, t1);
     fp12_frob(fp3, fp2_);
@@ -548,28 +647,30 @@ static BN_NI void final_exp(fp12* out, const fp12* in) {
     fp12_frob(fu2p, fu2);
     fp12_frob(fu3p, fu3);
     fp12_frob_p2(y2, fu2);
-    fp12_mul(y0, fp1, fp2_);
-    fp12_mul(y0, y0, fp3);
+    MUL(y0, fp1, fp2_);
+    MUL(y0, y0, fp3);
     fp12_conj(y1, t1);
     fp12_conj(y5, fu2);
     fp12_conj(y3, y3);
-    fp12_mul(y4, fu, fu2p);
+    MUL(y4, fu, fu2p);
     fp12_conj(y4, y4);
-    fp12_mul(y6, fu3, fu3p);
+    MUL(y6, fu3, fu3p);
     fp12_conj(y6, y6);
-    fp12_cyclo_sqr(t0, y6);
-    fp12_mul(t0, t0, y4);
-    fp12_mul(t0, t0, y5);
-    fp12_mul(t1, y3, y5);
-    fp12_mul(t1, t1, t0);
-    fp12_mul(t0, t0, y2);
-    fp12_cyclo_sqr(t1, t1);
-    fp12_mul(t1, t1, t0);
-    fp12_cyclo_sqr(t1, t1);
-    fp12_mul(t0, t1, y1);
-    fp12_mul(t1, t1, y0);
-    fp12_cyclo_sqr(t0, t0);
-    fp12_mul(*out, t0, t1);
+    CSQR(t0, y6);
+    MUL(t0, t0, y4);
+    MUL(t0, t0, y5);
+    MUL(t1, y3, y5);
+    MUL(t1, t1, t0);
+    MUL(t0, t0, y2);
+    CSQR(t1, t1);
+    MUL(t1, t1, t0);
+    CSQR(t1, t1);
+    MUL(t0, t1, y1);
+    MUL(t1, t1, y0);
+    CSQR(t0, t0);
+    MUL(*out, t0, t1);
+#undef MUL
+#undef CSQR
 }
 
 // ---------------------------------------------------------------- SoA helpers
@@ -788,16 +889,15 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ l
     fp12_store(fv, nlanes, c, f);
 }
 
-__global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
-                                                 const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv,
-                                                 uint32_t nlanes, uint8_t* __restrict__ verdict) {
-    uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchecks) return;
+// role/base as final_exp: the verdict is written by role 0
+GSV_DI void final_check(uint32_t c, const uint32_t* __restrict__ check_lane, const uint8_t* __restrict__ lstat,
+                        const uint32_t* __restrict__ fv, uint32_t nlanes, uint8_t* __restrict__ verdict, int role,
+                        int base) {
     uint32_t l0 = check_lane[c], l1 = check_lane[c + 1];
     bool bad = false;
     for (uint32_t l = l0; l < l1; l++) bad = bad || lstat[l] == CS_BAD;
     if (bad) {
-        verdict[c] = GSV_PAIRING_BAD_INPUT;
+        if (role == 0) verdict[c] = GSV_PAIRING_BAD_INPUT;
         return;
     }
     // product of the check's lane values; finalExponentiation(1) == 1 when no pair is finite
@@ -816,8 +916,26 @@ __global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ ch
     }
     if (!any) fp12_one(acc);
     fp12 r;
-    final_exp(&r, &acc);
-    verdict[c] = fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
+    final_exp(&r, &acc, role, base);
+    if (role == 0) verdict[c] = fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
+}
+
+__global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
+                                                 const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv,
+                                                 uint32_t nlanes, uint8_t* __restrict__ verdict) {
+    uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchecks) return;
+    final_check(c, check_lane, lstat, fv, nlanes, verdict, 0, -1);
+}
+// three lanes per check (21 triples per wave, lane 63 idle); a triple's lanes take the same path
+constexpr uint32_t FINAL3_PER_WAVE = 21;
+__global__ __launch_bounds__(64) void k_bn_final3(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
+                                                  const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv,
+                                                  uint32_t nlanes, uint8_t* __restrict__ verdict) {
+    int t = threadIdx.x / 3, role = threadIdx.x - 3 * t;
+    uint32_t c = blockIdx.x * FINAL3_PER_WAVE + t;
+    if (t >= (int)FINAL3_PER_WAVE || c >= nchecks) return;
+    final_check(c, check_lane, lstat, fv, nlanes, verdict, role, 3 * t);
 }
 
 
@@ -1043,8 +1161,9 @@ hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, u
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
                                 const uint32_t* d_check_lane, uint32_t nchecks, uint8_t* d_pstat, uint32_t* d_pts,
-                                uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv, uint8_t* d_verdict, hipStream_t st,
-                                void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx) {
+                                uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv, uint8_t* d_verdict, bool final3,
+                                hipStream_t st, void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
+                                void* tctx) {
     if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
         hipLaunchKernelGGL(bn::k_bn_prepare, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
@@ -1061,8 +1180,12 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
-        hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_lane, nchecks,
-                           d_lstat, d_fv, nlanes, d_verdict);
+        if (final3)
+            hipLaunchKernelGGL(bn::k_bn_final3, dim3((nchecks + bn::FINAL3_PER_WAVE - 1) / bn::FINAL3_PER_WAVE),
+                               dim3(64), 0, st, d_check_lane, nchecks, d_lstat, d_fv, nlanes, d_verdict);
+        else
+            hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_lane, nchecks,
+                               d_lstat, d_fv, nlanes, d_verdict);
         if (timer_end) timer_end(tctx, GSV_K_BN_FINAL);
     }
     return hipGetLastError();

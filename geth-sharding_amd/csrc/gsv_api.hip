@@ -647,7 +647,15 @@ struct BnTables {
     std::vector<uint32_t> lane_first;   // Miller lane l's pairs: pidx[lane_first[l] .. lane_first[l+1])
     std::vector<uint32_t> check_lane;   // check c's Miller lanes: [check_lane[c], check_lane[c+1])
     std::vector<uint8_t> bad_len;
+    bool final3 = false;                // final exponentiation on three cooperating lanes per check
 };
+// Final exponentiation layout: one lane per check is a ~10^4-product dependent chain; when the batch
+// gives the SIMDs fewer than one such wave each, three lanes per check share its exponentiations by
+// u (a third of the chain).  GSV_BN_FINAL3 = 0/1 forces the choice (A/B timing).
+static bool bn_final3(size_t nchecks, int cus) {
+    if (const char* e = getenv("GSV_BN_FINAL3")) return atoi(e) != 0;
+    return nchecks < (size_t)std::max(cus, 1) * 4 * 64;
+}
 // Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
 // lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
 // and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
@@ -723,6 +731,7 @@ static int bn_tables(const uint64_t* off, size_t n, uint64_t base, int cus, BnTa
     }
     t.check_lane[n] = (uint32_t)t.lane_first.size();
     t.lane_first.push_back((uint32_t)q);
+    t.final3 = bn_final3(n, cus);
     return GSV_SUCCESS;
 }
 static int device_cus(int device) {
@@ -757,7 +766,8 @@ static int bn_run(gsv_ctx* c, const uint8_t* d_in, const BnTables& t, size_t n, 
     HIPCHK(hipMemcpyAsync(d_clane, t.check_lane.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
     c->cur_stream = st;
     HIPCHK(gsv::launch_bn256_pairing(d_in, d_src, (uint32_t)np, d_lfirst, d_pidx, (uint32_t)nl, d_clane, (uint32_t)n,
-                                     d_pstat, d_pts, d_rs, d_lstat, d_fv, d_verdict, st, hook_begin, hook_end, c));
+                                     d_pstat, d_pts, d_rs, d_lstat, d_fv, d_verdict, t.final3, st, hook_begin,
+                                     hook_end, c));
     // errBadPairingInput for ragged lengths overrides the kernel's verdict (those checks had no pairs)
     static const uint8_t bad = GSV_PAIRING_BAD_INPUT;
     for (size_t i = 0; i < n; i++)

@@ -78,6 +78,18 @@ def test_pairing_random_batch_vs_oracle(ctx, oracle):
     assert set(want.tolist()) == {0, 1, 2}
 
 
+@pytest.mark.parametrize("final3", ["0", "1"])
+def test_pairing_final_exp_layout(ctx, oracle, monkeypatch, final3):
+    """One lane per check or three cooperating lanes (ds_bpermute exchanges, chosen for small
+    batches; GSV_BN_FINAL3 forces it): the same verdicts as the oracle either way, on batches whose
+    size is not a multiple of the 21 triples per wave."""
+    monkeypatch.setenv("GSV_BN_FINAL3", final3)
+    inputs = _random_inputs(oracle, 41)[:37]
+    out = ctx.pairing_check_batch(inputs)
+    want = np.array([_v(oracle, x) for x in inputs], np.uint8)
+    assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
+
+
 @pytest.mark.parametrize("k", [1, 2, 3, 4])
 def test_pairing_miller_lane_split(ctx, oracle, monkeypatch, k):
     """A check's pairs split over Miller lanes of <= k pairs (the host picks k from the batch size;

@@ -1,4 +1,5 @@
-"""A/B sweep of the pairing check's pairs-per-Miller-lane split (GSV_BN_PAIRS_PER_LANE) at the
+"""A/B sweep of the pairing check's pairs-per-Miller-lane split (GSV_BN_PAIRS_PER_LANE) and
+final-exponentiation layout (GSV_BN_FINAL3) at the
 configs[4] batch per GPU for N = 1, 2, 4, 8 ranks (65,536 / N checks).  Every run checks the
 verdicts against the generator's constructed truth.  Run on the GPU box from the repo root:
     python tools/pairing_sweep.py [checks ...]
@@ -14,13 +15,18 @@ import numpy as np
 import torch
 
 import gsv
+from gsv import _lib
 
 
-def run(ctx, n, k, reps=2):
+def run(ctx, n, k, f3=None, reps=2):
     if k:
         os.environ["GSV_BN_PAIRS_PER_LANE"] = str(k)
     else:
         os.environ.pop("GSV_BN_PAIRS_PER_LANE", None)
+    if f3 is not None:
+        os.environ["GSV_BN_FINAL3"] = str(f3)
+    else:
+        os.environ.pop("GSV_BN_FINAL3", None)
     pin = torch.empty((n, 768), dtype=torch.uint8, device="cuda")
     pexp = torch.empty((n,), dtype=torch.uint8, device="cuda")
     pver = torch.empty((n,), dtype=torch.uint8, device="cuda")
@@ -29,21 +35,27 @@ def run(ctx, n, k, reps=2):
     ctx.pairing_check_batch_dev(pin, off, pver)
     torch.cuda.synchronize()
     assert torch.equal(pver, pexp), "verdicts differ from the constructed truth"
+    ctx.reset_timing()
+    ctx.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(reps):
         ctx.pairing_check_batch_dev(pin, off, pver)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
-    return dt
+    ctx.set_timing(False)
+    ks = [ctx.kernel_time(k)[0] / reps for k in (_lib.K_BN_PREPARE, _lib.K_PAIRING, _lib.K_BN_FINAL)]
+    return dt, ks
 
 
 def main():
     sizes = [int(a) for a in sys.argv[1:]] or [65536, 32768, 16384, 8192]
     ctx = gsv.default_context()
     for n in sizes:
-        for k in (0, 1, 2, 4):
-            dt = run(ctx, n, k)
-            print(f"checks {n:6d} k {k or 'auto':>4}: {dt * 1e3:8.2f} ms  {n / dt / 1e6:.3f} M checks/s", flush=True)
+        for k, f3 in ((0, None), (1, None), (2, None), (4, None), (0, 0), (0, 1)):
+            dt, ks = run(ctx, n, k, f3)
+            print(f"checks {n:6d} k {k or 'auto':>4} final3 {'auto' if f3 is None else f3:>4}: {dt * 1e3:8.2f} ms  "
+                  f"{n / dt / 1e6:.3f} M checks/s  prepare/miller/final {ks[0]:.2f}/{ks[1]:.2f}/{ks[2]:.2f} ms",
+                  flush=True)
 
 
 if __name__ == "__main__":
