@@ -833,13 +833,15 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ l
         for (uint32_t q = b; q < e; q++) {
             uint32_t j = pidx[q];
             if (pstat[j] != PS_OK) continue;
-            g1a P;
-            soa_load(P.x, pts, npairs, j, 0);
-            soa_load(P.y, pts, npairs, j, 1);
-            g2j r;
-            g2j_load(r, rs, npairs, j);
 #pragma unroll 1
             for (int k = 0; k < (add ? 2 : 1); k++) {
+                // R and P are (re)loaded per line and R stored before the line product, so only
+                // f and the line are live across mul_line (the R reload hits L2)
+                g1a P;
+                soa_load(P.x, pts, npairs, j, 0);
+                soa_load(P.y, pts, npairs, j, 1);
+                g2j r;
+                g2j_load(r, rs, npairs, j);
                 if (k == 0) {
                     line_double_i(la, lb, lc, r, P);
                 } else {  // Q is only needed on the NAF's nonzero digits
@@ -853,9 +855,9 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ l
                     if (NAF_NEG & bit) fp2_neg(Q.y, Q.y);
                     line_add_i(la, lb, lc, r, Q, P, r2);
                 }
+                g2j_store(rs, npairs, j, r);
                 mul_line_i(f, la, lb, lc);
             }
-            g2j_store(rs, npairs, j, r);
         }
     }
     // Q1 = pi(Q), -Q2 = -pi^2(Q) (optate.go:168-209), per pair
