@@ -556,16 +556,16 @@ static BN_NI void line_double_p(fp2* pa, fp2* pb, fp2* pc, g2j* pr, const g1a* p
 GSV_DI void line_double(fp2& a, fp2& b, fp2& c, g2j& r, const g1a& q) { line_double_p(&a, &b, &c, &r, &q); }
 // optate.go:94-112
 GSV_DI void mul_line_i(fp12& ret, const fp2& a, const fp2& b, const fp2& c) {
-    // ordered so that at most ret + one F_p^6 temporary + the line are live at a time
-    fp6 s, a2;
+    // ordered (in place) so that at most ret + one F_p^6 temporary + the line are live at a time
+    fp6 a2;
     fp2 bc;
-    fp6_add(s, ret.x, ret.y);
-    fp6_mul_sparse_i(a2, ret.x, a, b);  // (0, a, b) * ret.x
+    fp6_mul_sparse_i(a2, ret.x, a, b);   // (0, a, b) * ret.x
+    fp6_add(ret.x, ret.x, ret.y);        // s = ret.x + ret.y
     fp6_mul_fp2_i(ret.y, ret.y, c);      // t3
     fp2_add(bc, b, c);
-    fp6_mul_sparse_i(s, s, a, bc);       // * (0, a, b + c)
-    fp6_sub(s, s, a2);
-    fp6_sub(ret.x, s, ret.y);
+    fp6_mul_sparse_i(ret.x, ret.x, a, bc);  // s * (0, a, b + c)
+    fp6_sub(ret.x, ret.x, a2);
+    fp6_sub(ret.x, ret.x, ret.y);
     fp6_mul_tau(a2, a2);
     fp6_add(ret.y, ret.y, a2);
 }
