@@ -64,3 +64,26 @@ def test_chunk_root_too_large(ctx):
     from gsv import GsvError
     with pytest.raises(GsvError):
         ctx.chunk_root_batch([b"\0" * ((1 << 20) + 1)])
+
+
+
+def test_chunk_root_dev_repeated(ctx, oracle):
+    """configs[2]-shaped device-resident batch (40 x 1 MiB): roots equal the oracle's and stay
+    stable over back-to-back calls on the context stream (workspace and cached offsets reused)."""
+    import torch
+    rng = np.random.default_rng(8)
+    n, L = 40, 1 << 20
+    h = rng.integers(0, 256, n * L, dtype=np.uint8)
+    d = torch.from_numpy(h).cuda()
+    off = np.arange(n + 1, dtype=np.uint64) * L
+    roots = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    first = None
+    for _ in range(3):
+        ctx.chunk_root_batch_dev(d, off, roots)
+        torch.cuda.synchronize()
+        r = roots.cpu().numpy().copy()
+        if first is None:
+            first = r
+        assert (r == first).all()
+    for i in (0, 19, 20, 39):
+        assert bytes(first[i]) == oracle.derive_sha_bytes(h[i * L:(i + 1) * L].tobytes()), i
