@@ -333,6 +333,33 @@ def main():
         stream.synchronize()
         barrier(ws)
         tdt = max_over_ranks(time.perf_counter() - t5, ws)
+        # Keccak-256 batch (crypto.Keccak256 over the same 400,000 tx RLP strings: the tx-hash /
+        # sighash workload, A10): one message per lane, offsets and data resident in HBM
+        koff_t = torch.from_numpy(voff.astype(np.int64)).to(dev)
+        kout = torch.empty((nblk * ntx, 32), dtype=torch.uint8, device=dev)
+        ctx.keccak256_batch_dev(vals, koff_t, kout, stream=stream)
+        stream.synchronize()
+        ksteps = 5
+        barrier(ws)
+        t8 = time.perf_counter()
+        for _ in range(ksteps):
+            ctx.keccak256_batch_dev(vals, koff_t, kout, stream=stream)
+        stream.synchronize()
+        barrier(ws)
+        kdt = max_over_ranks(time.perf_counter() - t8, ws)
+        if rank == 0 and not args.no_cpu_baseline:  # sample vs the oracle sponge
+            from oracle import oracle as O
+            hv = vals[:int(voff[64])].cpu().numpy().tobytes()
+            ko = kout[:64].cpu().numpy()
+            assert all(bytes(ko[i]) == O.keccak256(hv[int(voff[i]):int(voff[i + 1])]) for i in range(64)), \
+                "keccak256 batch mismatch vs oracle"
+        perms = int(np.sum(lens // 136 + 1))
+        extras["keccak256"] = {"hashes_per_s": round(ws * nblk * ntx * ksteps / kdt, 1),
+                               "GBps": round(ws * float(voff[-1]) * ksteps / kdt / 1e9, 3),
+                               "permutations_per_s": round(ws * perms * ksteps / kdt, 1),
+                               "messages": nblk * ntx, "bytes_per_message": "100-160",
+                               "ms_per_step": round(kdt / ksteps * 1e3, 3)}
+        del koff_t, kout
         extras["tx_root"] = {"blocks_per_s": round(ws * nblk * tsteps / tdt, 1),
                              "txs_per_s": round(ws * nblk * ntx * tsteps / tdt, 1),
                              "MBps_of_tx_rlp": round(ws * float(voff[-1]) * tsteps / tdt / 1e6, 1),

@@ -7,14 +7,28 @@
 
 namespace gsv {
 
-GSV_DI uint64_t load_le64_bytes(const uint8_t* p, uint32_t avail) {
-    // avail >= 8: full lane; otherwise partial (zero-filled)
-    uint64_t v = 0;
-    if (avail >= 8 && ((uintptr_t)p & 7u) == 0) return *(const uint64_t*)p;
+// One rate block (17 little-endian 64-bit words) of the message at p, `avail` bytes of it valid
+// (>= 136: a full block).  Messages sit at any byte offset (RLP strings packed back to back), so the
+// block is read as up to 35 aligned dwords from p rounded down to 4 and realigned with
+// v_alignbyte_b32 — 35 loads instead of 136 byte loads.  A dword is read only if it holds a valid
+// byte (so never past the page of the last one); bytes past `avail` are masked to zero.
+GSV_DI void load_block(uint64_t w[17], const uint8_t* p, uint32_t avail) {
+    const uint32_t* q = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+    uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    uint32_t take = avail < 136u ? avail : 136u;
+    uint32_t need = sh + take;  // bytes from q
+    uint32_t d[35];
 #pragma unroll
-    for (int b = 0; b < 8; b++)
-        if ((uint32_t)b < avail) v |= (uint64_t)p[b] << (8 * b);
-    return v;
+    for (int j = 0; j < 35; j++) d[j] = (4u * j < need) ? q[j] : 0u;
+#pragma unroll
+    for (int k = 0; k < 17; k++) {
+        uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * k + 1], d[2 * k], sh);
+        uint32_t hi = __builtin_amdgcn_alignbyte(d[2 * k + 2], d[2 * k + 1], sh);
+        uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        int32_t valid = (int32_t)take - 8 * k;
+        if (valid < 8) v = valid <= 0 ? 0 : v & ((1ull << (8 * valid)) - 1);
+        w[k] = v;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_keccak256(const uint8_t* __restrict__ data,
@@ -24,25 +38,26 @@ __global__ __launch_bounds__(256) void k_keccak256(const uint8_t* __restrict__ d
     if (i >= n) return;
     const uint8_t* p = data + off[i];
     uint64_t len = off[i + 1] - off[i];
-    uint64_t a[25];
+    uint64_t a[25], w[17];
 #pragma unroll
     for (int k = 0; k < 25; k++) a[k] = 0;
     while (len >= 136) {
+        load_block(w, p, 136);
 #pragma unroll
-        for (int k = 0; k < 17; k++) a[k] ^= load_le64_bytes(p + 8 * k, 8);
+        for (int k = 0; k < 17; k++) a[k] ^= w[k];
         keccakf(a);
         p += 136;
         len -= 136;
     }
     // final block: remaining len bytes, then 0x01 at len, 0x80 at 135
     uint32_t rem = (uint32_t)len;
+    load_block(w, p, rem);
 #pragma unroll
     for (int k = 0; k < 17; k++) {
-        int32_t avail = (int32_t)rem - 8 * k;
-        uint64_t w = avail > 0 ? load_le64_bytes(p + 8 * k, (uint32_t)(avail > 8 ? 8 : avail)) : 0;
-        if ((uint32_t)(rem >> 3) == (uint32_t)k) w ^= 0x01ull << (8 * (rem & 7u));
-        if (k == 16) w ^= 0x8000000000000000ULL;
-        a[k] ^= w;
+        uint64_t x = w[k];
+        if ((uint32_t)(rem >> 3) == (uint32_t)k) x ^= 0x01ull << (8 * (rem & 7u));
+        if (k == 16) x ^= 0x8000000000000000ULL;
+        a[k] ^= x;
     }
     keccakf(a);
     uint8_t* o = out32 + (size_t)i * 32;
