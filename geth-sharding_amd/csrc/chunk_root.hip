@@ -941,7 +941,8 @@ hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies,
 
 // ================================================================ generic DeriveSha (any DerivableList)
 // RLP length prefix for a string (base 0x80) or list (base 0xc0) of `len` bytes (rlp/encode.go:71-89)
-GSV_DI void put_prefix(Writer& w, uint8_t base, uint32_t len) {
+template <class W>
+GSV_DI void put_prefix(W& w, uint8_t base, uint32_t len) {
     if (len < 56) {
         w.put((uint8_t)(base + len));
         return;
@@ -952,6 +953,68 @@ GSV_DI void put_prefix(Writer& w, uint8_t base, uint32_t len) {
 }
 GSV_DI uint32_t prefix_len(uint32_t len) {
     return len < 56 ? 1u : len < 256 ? 2u : len < 65536 ? 3u : len < (1u << 24) ? 4u : 5u;
+}
+
+// A leaf's RLP header (<= 16 bytes) assembled in two registers, byte n at bits 8n
+struct RegWriter {
+    uint64_t w0 = 0, w1 = 0;
+    uint32_t n = 0;
+    GSV_DI void put(uint8_t b) {
+        if (n < 8) w0 |= (uint64_t)b << (8 * n);
+        else if (n < 16) w1 |= (uint64_t)b << (8 * (n - 8));
+        n++;
+    }
+    GSV_DI void str(const uint8_t* s, int len) {  // RLP string, len < 56 (as Writer::str)
+        if (len == 1 && s[0] < 0x80) {
+            put(s[0]);
+            return;
+        }
+        put((uint8_t)(0x80 + len));
+        for (int k = 0; k < len; k++) put(s[k]);
+    }
+};
+GSV_DI uint64_t low_bytes(int32_t n) { return n <= 0 ? 0ull : n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1ull); }
+// Keccak-256 of header(H bytes in hw0/hw1) || v[0..L) without materialising the message: each rate
+// block is read from v as <= 35 aligned dwords (only those holding a value byte) realigned with
+// v_alignbyte, bytes outside the value masked, the header OR-ed into block 0's first two words.
+GSV_DI void keccak_hdr_value(uint32_t h[8], uint64_t hw0, uint64_t hw1, uint32_t H, const uint8_t* v, uint32_t L) {
+    uint64_t a[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) a[k] = 0;
+    uint32_t len = H + L, nfull = len / 136;
+    for (uint32_t blk = 0; blk <= nfull; blk++) {
+        int32_t base = (int32_t)(136 * blk);
+        int32_t vlo = max((int32_t)H - base, 0), vhi = min((int32_t)len - base, 136);
+        uintptr_t sa = (uintptr_t)v - H + (uintptr_t)base;  // source of block byte 0 (value coordinates)
+        const uint32_t* q = (const uint32_t*)(sa & ~(uintptr_t)3);
+        uint32_t sh = (uint32_t)(sa & 3u);
+        uint32_t d[35];
+#pragma unroll
+        for (int j = 0; j < 35; j++) {
+            int32_t b0 = 4 * j - (int32_t)sh;  // block position of dword j's first byte
+            d[j] = (b0 + 4 > vlo && b0 < vhi) ? q[j] : 0u;
+        }
+        int32_t rem = (int32_t)len - base;  // in the final block: position of the 0x01 pad byte
+#pragma unroll
+        for (int k = 0; k < 17; k++) {
+            uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * k + 1], d[2 * k], sh);
+            uint32_t hi = __builtin_amdgcn_alignbyte(d[2 * k + 2], d[2 * k + 1], sh);
+            uint64_t x = ((uint64_t)lo | ((uint64_t)hi << 32)) & low_bytes(vhi - 8 * k) & ~low_bytes(vlo - 8 * k);
+            if (blk == 0 && k == 0) x |= hw0;
+            if (blk == 0 && k == 1) x |= hw1;
+            if (blk == nfull) {
+                if ((rem >> 3) == k) x ^= 0x01ull << (8 * (rem & 7));
+                if (k == 16) x ^= 0x8000000000000000ULL;
+            }
+            a[k] ^= x;
+        }
+        keccakf(a);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        h[2 * k] = (uint32_t)a[k];
+        h[2 * k + 1] = (uint32_t)(a[k] >> 32);
+    }
 }
 
 // One lane per leaf: leaf j of list b = shortNode{hexToCompact(key(j)[depth:]), valueNode(GetRlp(j))}
@@ -975,6 +1038,20 @@ __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__
     uint32_t kenc = (cl == 1 && ck[0] < 0x80) ? 1u : 1u + cl;
     bool vbyte = (L == 1 && v[0] < 0x80);
     uint32_t venc = vbyte ? 1u : prefix_len(L) + L;
+    uint8_t* s = leafrefs + item * REF_STRIDE;
+    if (!vbyte) {  // hashed leaves (>= 32 bytes or the root): header in registers, value read in place
+        RegWriter r;
+        put_prefix(r, 0xc0, kenc + venc);
+        r.str(ck, cl);
+        put_prefix(r, 0x80, L);
+        if (r.n <= 16 && (N == 1 || r.n + L >= 32)) {
+            uint32_t h[8];
+            keccak_hdr_value(h, r.w0, r.w1, r.n, v, L);
+            if (N == 1) store_hash32(roots + (size_t)b * 32, h);
+            else store_hashref_slot(s, h);
+            return;
+        }
+    }
     // this item's message buffer: 8-byte aligned, disjoint from its neighbours' (each needs <= L + 17
     // bytes and starts at least L + 25 bytes after the previous one)
     uint8_t* m = lmsg + (((voff[item] - voff[0]) + 7) & ~7ull) + 32ull * item;
@@ -988,7 +1065,6 @@ __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__
         for (uint32_t k = 0; k < L; k++) w.put(v[k]);
     }
     uint32_t len = w.n;
-    uint8_t* s = leafrefs + item * REF_STRIDE;
     if (N == 1 || len >= 32) {
         uint32_t h[8];
         keccak_buf(h, m, len);
