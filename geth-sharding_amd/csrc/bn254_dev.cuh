@@ -15,6 +15,7 @@
 
 #define GSV_DI __device__ __forceinline__
 
+#include "modinv30.cuh"
 #include "mul_asm.cuh"
 
 namespace gsv {
@@ -189,16 +190,16 @@ static BN_NI v8 fp_mul_v(v8 a, v8 b) {
 }
 GSV_DI void fp_mul_c(fp& r, const fp& a, const fp& b) { r = fromv(fp_mul_v(tov(a), tov(b))); }
 GSV_DI void fp_sqr_c(fp& r, const fp& a) { fp_mul_c(r, a, a); }
-// a^(p-2) (gfp.go:31-49 computes the same canonical residue)
+// Inverse of a Montgomery residue aR: safegcd (modinv30.cuh, ~8k issue slots) gives (aR)^-1 =
+// a^-1 R^-1, and one Montgomery product by R^3 mod p turns it into a^-1 R — the same canonical
+// residue as the reference's a^(p-2) (gfp.go:31-49), whose 254 squarings + 127 products it replaces.
+__device__ constexpr uint32_t BN_R3[8] = {0xda1530dfu, 0xb1cd6dafu, 0xa7283db6u, 0x62f210e6u,
+                                          0x0ada0afbu, 0xef7f0b0cu, 0x2d592544u, 0x20fd6e90u};
 GSV_DI void fp_inv(fp& r, const fp& a) {
-    fp s, pw = a;
-    fp_const(s, BN_ONE);
-#pragma unroll 1
-    for (int b = 0; b < 254; b++) {
-        if ((BN_PM2[b >> 5] >> (b & 31)) & 1u) fp_mul_c(s, s, pw);
-        fp_sqr_c(pw, pw);
-    }
-    r = s;
+    fp t, r3;
+    modinv30_words(t.v, a.v, MI30_BN);
+    fp_const(r3, BN_R3);
+    fp_mul_c(r, t, r3);
 }
 
 // ---------------------------------------------------------------- F_p^2 (gfp2.go)

@@ -1,5 +1,6 @@
 // Constant-time modular inversion by Bernstein-Yang "safegcd" divsteps (20 batches of 30
-// divsteps, signed 30-bit limbs), for the secp256k1 group order n and field prime p.
+// divsteps, signed 30-bit limbs), for the secp256k1 group order n and field prime p and the BN254
+// base field prime.
 //
 // Why: the Fermat inversions it replaces cost ~255 squarings + ~15-75 products each (the scalar
 // one in 8 x 32-bit carry-chain arithmetic: ~16 % of k_ecrecover).  A divstep is ~19 plain
@@ -36,6 +37,9 @@ MI30_CONST modinfo30 MI30_N = {{0x10364141, 0x3F497A33, 0x348A03BB, 0x2BB739AB, 
                                 0x3FFFFFFF, 0x3FFFFFFF, 0xFFFF}, 0x2A774EC1u};
 MI30_CONST modinfo30 MI30_P = {{0x3FFFFC2F, 0x3FFFFFFB, 0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF,
                                 0x3FFFFFFF, 0x3FFFFFFF, 0xFFFF}, 0x2DDACACFu};
+// the BN254 base field prime (crypto/bn256/cloudflare/constants.go:22), for F_p inversions
+MI30_CONST modinfo30 MI30_BN = {{0x187CFD47, 0x3082305B, 0x071CA8D3, 0x205AA45A, 0x01585D97, 0x0116DA06,
+                                 0x1A029B85, 0x139CB84C, 0x00003064}, 0x1B799C77u};
 
 constexpr int32_t MI30_M30 = 0x3FFFFFFF;
 

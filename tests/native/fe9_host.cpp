@@ -43,4 +43,4 @@ void h_build_table(uint32_t* T, uint32_t* zfac, const uint32_t* x, const uint32_
 }
 }
 #include "../../geth-sharding_amd/csrc/modinv30.cuh"
-extern "C" void h_modinv(uint32_t* out, const uint32_t* x, int which) { modinv30_words(out, x, which ? MI30_P : MI30_N); }
+extern "C" void h_modinv(uint32_t* out, const uint32_t* x, int which) { modinv30_words(out, x, which == 2 ? MI30_BN : which ? MI30_P : MI30_N); }

@@ -271,13 +271,14 @@ def test_build_r_table(lib):
 
 
 N_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+BN_P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
 
 
 def test_safegcd_modinv(lib):
-    """modinv30.cuh (Bernstein-Yang divsteps) against pow(x, -1, m) for m = n and m = p."""
+    """modinv30.cuh (Bernstein-Yang divsteps) against pow(x, -1, m) for m = n, p and the BN254 prime."""
     rng = random.Random(20)
     W8 = ctypes.c_uint32 * 8
-    for which, m in ((0, N_ORDER), (1, P)):
+    for which, m in ((0, N_ORDER), (1, P), (2, BN_P)):
         xs = [0, 1, 2, 3, m - 1, m - 2, (m - 1) // 2, 2**255, 2**128 + 1, 0xFFFFFFFF] + [rng.randrange(1, m) for _ in range(3000)]
         xs += [rng.getrandbits(rng.randrange(1, 256)) % m for _ in range(500)]
         for x in xs:
