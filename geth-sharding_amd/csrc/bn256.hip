@@ -245,7 +245,7 @@ static BN_NI void fp12_mul3(fp12* pe, const fp12* pa, const fp12* pb, int role, 
     fp6_add(sb, b.x, b.y);
     l = role == 0 ? a.x : role == 1 ? a.y : sa;
     r = role == 0 ? b.x : role == 1 ? b.y : sb;
-    fp6_mul(prod, l, r);
+    fp6_mul_i(prod, l, r);
     gather3(v, prod, base);
     fp6_sub(tx, v[2], v[0]);
     fp6_sub(tx, tx, v[1]);
