@@ -301,9 +301,8 @@ GSV_DI void g2_double_i(g2j& c, const g2j& pa_) {
 static BN_NI void g2_double_p(g2j* pc, const g2j* pa) { g2_double_i(*pc, *pa); }
 GSV_DI void g2_double(g2j& c, const g2j& a) { g2_double_p(&c, &a); }
 // twist.go:73-134 add-2007-bl with its infinity / doubling cases
-static BN_NI void g2_add_p(g2j* pc, const g2j* pa, const g2j* pb) {
-    const g2j a = *pa, b = *pb;
-    g2j& c = *pc;
+GSV_DI void g2_add_i(g2j& c, const g2j& pa_, const g2j& pb_) {
+    const g2j a = pa_, b = pb_;
     if (fp2_is_zero(a.z)) { c = b; return; }
     if (fp2_is_zero(b.z)) { c = a; return; }
     fp2 z12, z22, u1, u2, t, s1, s2, h, i, j, r, v, t4, t6;
@@ -343,6 +342,7 @@ static BN_NI void g2_add_p(g2j* pc, const g2j* pa, const g2j* pb) {
     o.t = a.t;
     c = o;
 }
+static BN_NI void g2_add_p(g2j* pc, const g2j* pa, const g2j* pb) { g2_add_i(*pc, *pa, *pb); }
 GSV_DI void g2_add(g2j& c, const g2j& a, const g2j& b) { g2_add_p(&c, &a, &b); }
 // c = a + q with q affine (z = 1): madd-2007-bl, 8M + 3S instead of the general 11M + 5S.  Used only
 // inside the subgroup predicate, whose boolean outcome does not depend on the formulas chosen.
@@ -436,17 +436,17 @@ GSV_DI bool g2_in_subgroup(const g2a* q) {
         if (pos || neg) g2_add_mixed_i(uq, uq, neg ? mq : *q);
     }
     g2j lhs, p1, p2, rhs, tmp;
-    g2_add(lhs, uq, a);          // [u+1]Q
+    g2_add_i(lhs, uq, a);          // [u+1]Q
     g2_psi(p1, uq);              // psi([u]Q)
     g2_psi(p2, p1);              // psi^2([u]Q)
-    g2_add(lhs, lhs, p1);
-    g2_add(lhs, lhs, p2);
-    g2_double(tmp, uq);          // [2u]Q
+    g2_add_i(lhs, lhs, p1);
+    g2_add_i(lhs, lhs, p2);
+    g2_double_i(tmp, uq);          // [2u]Q
     g2_psi(rhs, tmp);
     g2_psi(rhs, rhs);
     g2_psi(rhs, rhs);            // psi^3([2u]Q)
     fp2_neg(rhs.y, rhs.y);
-    g2_add(tmp, lhs, rhs);       // lhs - rhs
+    g2_add_i(tmp, lhs, rhs);       // lhs - rhs
     return fp2_is_zero(tmp.z);
 }
 
@@ -715,7 +715,11 @@ GSV_DI bool fp_unmarshal(fp& r, const uint8_t* p) {
 // ---------------------------------------------------------------- kernels
 enum : uint8_t { PS_OK = 0, PS_SKIP = 1, PS_BAD = 2 };
 
-__global__ __launch_bounds__(64) void k_bn_prepare(const uint8_t* __restrict__ in,
+// Two waves per SIMD (a 256-register budget: the subgroup loop spills ~160 VGPRs to scratch) beat
+// one wave with everything in registers: simple VALU ops issue at twice the rate with a second
+// wave (profiles/r01_microbench_lat.txt), and a full batch has 4 waves of pairs per SIMD.
+// Measured 7.8 -> 6.4 ms per 262,144 pairs.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_bn_prepare(const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ pair_src,
                                                    uint32_t npairs, uint8_t* __restrict__ pstat,
                                                    uint32_t* __restrict__ pts /* [48 words][npairs] */) {
