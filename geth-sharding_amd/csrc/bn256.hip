@@ -897,11 +897,13 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ l
 }
 
 // role/base as final_exp: the verdict is written by role 0
-GSV_DI void final_check(uint32_t c, const uint32_t* __restrict__ check_lane, const uint8_t* __restrict__ lstat,
-                        const uint32_t* __restrict__ fv, uint32_t nlanes, uint8_t* __restrict__ verdict, int role,
-                        int base) {
+// cbad[c] != 0: the check's input length is not a multiple of 192 (errBadPairingInput,
+// core/vm/contracts.go:336-338); it has no pairs
+GSV_DI void final_check(uint32_t c, const uint32_t* __restrict__ check_lane, const uint8_t* __restrict__ cbad,
+                        const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv, uint32_t nlanes,
+                        uint8_t* __restrict__ verdict, int role, int base) {
     uint32_t l0 = check_lane[c], l1 = check_lane[c + 1];
-    bool bad = false;
+    bool bad = cbad[c] != 0;
     for (uint32_t l = l0; l < l1; l++) bad = bad || lstat[l] == CS_BAD;
     if (bad) {
         if (role == 0) verdict[c] = GSV_PAIRING_BAD_INPUT;
@@ -928,21 +930,23 @@ GSV_DI void final_check(uint32_t c, const uint32_t* __restrict__ check_lane, con
 }
 
 __global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
-                                                 const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv,
-                                                 uint32_t nlanes, uint8_t* __restrict__ verdict) {
+                                                 const uint8_t* __restrict__ cbad, const uint8_t* __restrict__ lstat,
+                                                 const uint32_t* __restrict__ fv, uint32_t nlanes,
+                                                 uint8_t* __restrict__ verdict) {
     uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchecks) return;
-    final_check(c, check_lane, lstat, fv, nlanes, verdict, 0, -1);
+    final_check(c, check_lane, cbad, lstat, fv, nlanes, verdict, 0, -1);
 }
 // three lanes per check (21 triples per wave, lane 63 idle); a triple's lanes take the same path
 constexpr uint32_t FINAL3_PER_WAVE = 21;
 __global__ __launch_bounds__(64) void k_bn_final3(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
-                                                  const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv,
-                                                  uint32_t nlanes, uint8_t* __restrict__ verdict) {
+                                                  const uint8_t* __restrict__ cbad, const uint8_t* __restrict__ lstat,
+                                                  const uint32_t* __restrict__ fv, uint32_t nlanes,
+                                                  uint8_t* __restrict__ verdict) {
     int t = threadIdx.x / 3, role = threadIdx.x - 3 * t;
     uint32_t c = blockIdx.x * FINAL3_PER_WAVE + t;
     if (t >= (int)FINAL3_PER_WAVE || c >= nchecks) return;
-    final_check(c, check_lane, lstat, fv, nlanes, verdict, role, 3 * t);
+    final_check(c, check_lane, cbad, lstat, fv, nlanes, verdict, role, 3 * t);
 }
 
 
@@ -1167,10 +1171,10 @@ hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, u
 
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
-                                const uint32_t* d_check_lane, uint32_t nchecks, uint8_t* d_pstat, uint32_t* d_pts,
-                                uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv, uint8_t* d_verdict, bool final3,
-                                hipStream_t st, void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
-                                void* tctx) {
+                                const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
+                                uint8_t* d_pstat, uint32_t* d_pts, uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv,
+                                uint8_t* d_verdict, bool final3, hipStream_t st, void (*timer_begin)(void*, int),
+                                void (*timer_end)(void*, int), void* tctx) {
     if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
         hipLaunchKernelGGL(bn::k_bn_prepare, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
@@ -1189,10 +1193,10 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
         if (final3)
             hipLaunchKernelGGL(bn::k_bn_final3, dim3((nchecks + bn::FINAL3_PER_WAVE - 1) / bn::FINAL3_PER_WAVE),
-                               dim3(64), 0, st, d_check_lane, nchecks, d_lstat, d_fv, nlanes, d_verdict);
+                               dim3(64), 0, st, d_check_lane, nchecks, d_cbad, d_lstat, d_fv, nlanes, d_verdict);
         else
             hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_lane, nchecks,
-                               d_lstat, d_fv, nlanes, d_verdict);
+                               d_cbad, d_lstat, d_fv, nlanes, d_verdict);
         if (timer_end) timer_end(tctx, GSV_K_BN_FINAL);
     }
     return hipGetLastError();

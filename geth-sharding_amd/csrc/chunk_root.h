@@ -79,19 +79,35 @@ struct TriePlan {
     PNode* d_nodes = nullptr;
     PChild* d_children = nullptr;
     uint16_t* d_leaf_depth = nullptr;
+    size_t bytes = 0;  // host + device footprint
+    TriePlan() = default;
+    TriePlan(const TriePlan&) = delete;
+    TriePlan& operator=(const TriePlan&) = delete;
+    ~TriePlan();  // frees the device arrays (also on a failed, partial upload)
 };
 
 void build_trie_plan(TriePlanHost& p, uint32_t N, bool generic = false);
 
+// Per-(N, generic) plans, built and uploaded on first use.  Bounded: beyond kMaxBytes the
+// least-recently-used plans that no prepared shape holds (use_count == 1: no queued work can read
+// them, because a shape drains its work before it is dropped) are freed.
 class PlanCache {
   public:
-    ~PlanCache();
-    // returns a device-resident plan for length N (built and uploaded on first use)
-    TriePlan* get(uint32_t N, bool generic = false);
+    static constexpr size_t kMaxBytes = (size_t)512 << 20;
+    // nullptr when the device upload fails (out of memory)
+    std::shared_ptr<TriePlan> get(uint32_t N, bool generic = false);
+    size_t bytes() const { return bytes_; }
+    size_t size() const { return plans_.size(); }
 
   private:
+    struct Entry {
+        std::shared_ptr<TriePlan> plan;
+        uint64_t last_use;
+    };
     std::mutex mu_;
-    std::map<uint64_t, std::unique_ptr<TriePlan>> plans_;
+    std::map<uint64_t, Entry> plans_;
+    uint64_t tick_ = 0;
+    size_t bytes_ = 0;
 };
 
 }  // namespace gsv

@@ -241,42 +241,53 @@ void build_trie_plan(TriePlanHost& p, uint32_t N, bool generic) {
     }
 }
 
-PlanCache::~PlanCache() {
-    for (auto& kv : plans_) {
-        if (kv.second->d_nodes) (void)hipFree(kv.second->d_nodes);
-        if (kv.second->d_children) (void)hipFree(kv.second->d_children);
-        if (kv.second->d_leaf_depth) (void)hipFree(kv.second->d_leaf_depth);
-    }
+TriePlan::~TriePlan() {
+    if (d_nodes) (void)hipFree(d_nodes);
+    if (d_children) (void)hipFree(d_children);
+    if (d_leaf_depth) (void)hipFree(d_leaf_depth);
 }
 
-TriePlan* PlanCache::get(uint32_t N, bool generic) {
+template <typename T>
+static bool upload(T** dst, const std::vector<T>& src) {
+    if (src.empty()) return true;
+    size_t nb = src.size() * sizeof(T);
+    if (hipMalloc(dst, nb) != hipSuccess) {
+        *dst = nullptr;
+        return false;
+    }
+    return hipMemcpy(*dst, src.data(), nb, hipMemcpyHostToDevice) == hipSuccess;
+}
+
+std::shared_ptr<TriePlan> PlanCache::get(uint32_t N, bool generic) {
     std::lock_guard<std::mutex> g(mu_);
     uint64_t key = (uint64_t)N | (generic ? (1ull << 32) : 0ull);
     auto it = plans_.find(key);
-    if (it != plans_.end()) return it->second.get();
-    auto pl = std::make_unique<TriePlan>();
+    if (it != plans_.end()) {
+        it->second.last_use = ++tick_;
+        return it->second.plan;
+    }
+    auto pl = std::make_shared<TriePlan>();
     build_trie_plan(pl->h, N, generic);
-    if (!pl->h.leaf_depth.empty()) {
-        size_t nb = pl->h.leaf_depth.size() * sizeof(uint16_t);
-        if (hipMalloc(&pl->d_leaf_depth, nb) != hipSuccess) return nullptr;
-        if (hipMemcpy(pl->d_leaf_depth, pl->h.leaf_depth.data(), nb, hipMemcpyHostToDevice) != hipSuccess)
-            return nullptr;
+    // a failed upload returns nullptr; the destructor frees whatever was allocated
+    if (!upload(&pl->d_leaf_depth, pl->h.leaf_depth) || !upload(&pl->d_nodes, pl->h.nodes) ||
+        !upload(&pl->d_children, pl->h.children))
+        return nullptr;
+    pl->bytes = 2 * (pl->h.leaf_depth.size() * sizeof(uint16_t) + pl->h.nodes.size() * sizeof(PNode) +
+                     pl->h.children.size() * sizeof(PChild));
+    bytes_ += pl->bytes;
+    plans_[key] = Entry{pl, ++tick_};
+    // evict least-recently-used plans nobody else holds
+    while (bytes_ > kMaxBytes) {
+        auto victim = plans_.end();
+        for (auto e = plans_.begin(); e != plans_.end(); ++e)
+            if (e->first != key && e->second.plan.use_count() == 1 &&
+                (victim == plans_.end() || e->second.last_use < victim->second.last_use))
+                victim = e;
+        if (victim == plans_.end()) break;
+        bytes_ -= victim->second.plan->bytes;
+        plans_.erase(victim);
     }
-    if (!pl->h.nodes.empty()) {
-        if (hipMalloc(&pl->d_nodes, pl->h.nodes.size() * sizeof(PNode)) != hipSuccess) return nullptr;
-        if (hipMemcpy(pl->d_nodes, pl->h.nodes.data(), pl->h.nodes.size() * sizeof(PNode),
-                      hipMemcpyHostToDevice) != hipSuccess)
-            return nullptr;
-        if (!pl->h.children.empty()) {
-            if (hipMalloc(&pl->d_children, pl->h.children.size() * sizeof(PChild)) != hipSuccess) return nullptr;
-            if (hipMemcpy(pl->d_children, pl->h.children.data(), pl->h.children.size() * sizeof(PChild),
-                          hipMemcpyHostToDevice) != hipSuccess)
-                return nullptr;
-        }
-    }
-    TriePlan* r = pl.get();
-    plans_[key] = std::move(pl);
-    return r;
+    return pl;
 }
 
 // ================================================================ device side

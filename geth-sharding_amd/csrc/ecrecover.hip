@@ -16,8 +16,9 @@
 //     {1,3,5,7}R built on an isomorphic curve (libsecp-style "global z") so all table points are
 //     affine without an inversion, lambda-table x-coordinates precomputed (x * beta).
 //     129 doublings + 88 mixed additions.
-//   * u1*G: fixed-base comb, 32 byte-wide windows from a 522 KiB affine table in HBM (L2-resident),
-//     32 mixed additions and no doublings.
+//   * u1*G: fixed-base comb, 16 windows of 16 bits from an 80 MiB affine table in HBM (Infinity-Cache
+//     resident, one random 80-byte entry per window, prefetched a window ahead), 16 mixed additions
+//     and no doublings (gsv_internal.h COMB_BITS).
 //   * one general Jacobian add to combine, one field inversion to affine, fused Keccak-256 address.
 #include "recover_dev.cuh"
 
@@ -70,7 +71,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     load32_be(r, r32 + (size_t)i * 32);
     load32_be(s, s32 + (size_t)i * 32);
     uint8_t V = (uint8_t)(v[i] - 27u);  // byte(Vb.Uint64() - 27)
-    bool valid = vbig[i] == 0;
+    // Vb.BitLen() > 8 -> ErrInvalidSig, whatever the caller's v_big flag says
+    bool valid = vbig[i] == 0 && v[i] <= 0xFFu;
     sc rs, ss;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -85,6 +87,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     if (!valid) st = GSV_ST_INVALID_SIG;
     store_pub_addr(nullptr, addr20 + (size_t)i * 20, st == GSV_ST_OK, qx, qy);
     status[i] = (uint8_t)st;
+}
+
+// The ecrecover precompile (core/vm/contracts.go:78-101): input = hash(32) || v(32) || r(32) || s(32),
+// right-padded to 128 bytes by the caller (common.RightPadBytes).  ok[i] = 1 and out32 = the
+// left-padded signer address (LeftPadBytes(Keccak256(pub[1:])[12:], 32)) on success; ok[i] = 0 and
+// out32 zero where the reference returns (nil, nil): input[32:63] not all zero, or
+// ValidateSignatureValues(v - 27, r, s, homestead = false) false, or Ecrecover failing.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAVES, GSV_ECR_WAVES))) void k_ecrecover_precompile(
+    const uint8_t* __restrict__ in128, uint32_t n, const uint4* __restrict__ gtab, uint8_t* __restrict__ out32,
+    uint8_t* __restrict__ ok) {
+    __shared__ uint32_t ltab[GSV_LTAB_WORDS];
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* p = in128 + (size_t)i * 128;
+    uint32_t msg[8], r[8], s[8];
+    load32_be(msg, p);
+    load32_be(r, p + 64);
+    load32_be(s, p + 96);
+    uint32_t hi = 0;  // allZero(input[32:63])
+#pragma unroll
+    for (int k = 32; k < 63; k++) hi |= p[k];
+    uint8_t V = (uint8_t)(p[63] - 27u);  // byte arithmetic, wraps like the reference
+    sc rs, ss;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        rs.v[k] = r[k];
+        ss.v[k] = s[k];
+    }
+    bool valid = hi == 0 && !sc_is_zero(rs) && !sc_is_zero(ss) && limbs_lt(r, SN) && limbs_lt(s, SN) &&
+                 (V == 0 || V == 1);
+    fe qx, qy;
+    uint32_t st = recover_core(qx, qy, msg, r, s, V & 1u, gtab, ltab + threadIdx.x);
+    bool good = valid && st == GSV_ST_OK;
+    uint8_t* o = out32 + (size_t)i * 32;
+#pragma unroll
+    for (int k = 0; k < 12; k++) o[k] = 0;
+    store_pub_addr(nullptr, o + 12, good, qx, qy);
+    ok[i] = good ? 1 : 0;
 }
 
 // Fixed-base comb table: entry (w, d) = d * 2^(COMB_BITS w) * G, affine, canonical fe9 limbs
@@ -185,6 +225,13 @@ hipError_t launch_sender(const uint8_t* sighash32, const uint8_t* r32, const uin
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_sender, dim3((n + 255) / 256), dim3(256), 0, st, sighash32, r32, s32, v, vbig,
                        n, homestead, gtab, addr20, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_ecrecover_precompile(const uint8_t* in128, uint32_t n, const uint4* gtab, uint8_t* out32,
+                                       uint8_t* ok, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ecrecover_precompile, dim3((n + 255) / 256), dim3(256), 0, st, in128, n, gtab, out32, ok);
     return hipGetLastError();
 }
 

@@ -1,14 +1,23 @@
 // C ABI of libgsv.so (include/gsv.h): context, device memory staging, launches, timing.
-// Host-pointer entry points stage through a grow-only device arena on the context's stream;
-// *_dev entry points take HBM-resident buffers and the caller's stream and never allocate or
-// synchronize (graph-capturable).
+//
+// Host-pointer entry points stage through a grow-only device arena on the context's stream and are
+// synchronous.  *_dev entry points take HBM-resident buffers and the caller's stream and only
+// enqueue: they never allocate and never synchronize, so they can be captured into a HIP graph.
+// Everything a *_dev call derives from its host-side arguments (trie plans per body length, device
+// copies of offset tables, pairing lane tables, its workspace) lives in a PREPARED SHAPE built by the
+// matching gsv_*_prepare call (which may allocate and synchronize) and cached per context, keyed by
+// exactly those host-side arguments.  A *_dev call whose shape was not prepared returns
+// GSV_E_NOT_PREPARED without touching the device.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <list>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -16,6 +25,94 @@
 #include "chunk_root.h"
 #include "gsv_internal.h"
 #include "tx_host.h"
+
+namespace {
+
+size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// regions of one device allocation (256-B aligned offsets)
+struct Layout {
+    size_t n = 0;
+    size_t add(size_t bytes) {
+        size_t o = n;
+        n += al(bytes ? bytes : 1);
+        return o;
+    }
+};
+
+enum ShapeKind : uint64_t { SK_CHUNK = 1, SK_PAIRING = 2, SK_NOTARY = 3, SK_DERIVE = 4, SK_POC = 5, SK_HEADER = 6 };
+
+// scatter run: roots of group positions [from, from + count) go to output indices [dst, dst + count)
+struct Run { uint32_t dst, from, count; };
+
+// one launch of the trie-plan kernels over the bodies (or lists) of one length
+struct TrieGroup {
+    std::shared_ptr<gsv::TriePlan> plan;
+    uint32_t count = 0;
+    size_t koff = 0;      // chunk: first entry in the body-offset table
+    bool direct = false;  // chunk: roots written in place (one group holding bodies 0..n-1 in order)
+    size_t o_roots = 0, o_scr = 0, o_base = 0;
+    std::vector<Run> runs;
+};
+
+// chunk roots of a set of bodies (d_bodies[start[i] .. end[i]))
+struct ChunkLaunch {
+    std::vector<TrieGroup> groups;
+    std::vector<uint32_t> empty;  // zero-length bodies -> emptyRoot
+    size_t o_off = 0, o_empty = 0;
+};
+
+struct Shape {
+    uint64_t kind = 0;
+    std::vector<uint64_t> key;
+    uint8_t* mem = nullptr;
+    size_t bytes = 0;
+    bool owned = true;  // false: carved from the host-path arena
+    hipEvent_t ev = nullptr;     // recorded after the last (non-captured) use
+    hipStream_t last = nullptr;  // stream of that use
+    std::vector<std::pair<size_t, std::vector<uint8_t>>> uploads;  // host tables, copied at prepare
+    ChunkLaunch chunk;  // SK_CHUNK, SK_NOTARY, SK_POC
+    // SK_PAIRING
+    size_t np = 0, nl = 0, nchecks = 0;
+    bool final3 = false;
+    size_t o_src = 0, o_pidx = 0, o_lfirst = 0, o_clane = 0, o_cbad = 0, o_pstat = 0, o_pts = 0, o_rs = 0,
+           o_lstat = 0, o_fv = 0;
+    // SK_NOTARY
+    uint32_t max_txs = 0, sfx_len = 0;
+    int signer_kind = 0;
+    size_t o_cid = 0, o_noff = 0, o_nlen = 0, o_cnt = 0, o_blobs = 0;
+    // SK_DERIVE
+    std::vector<TrieGroup> dgroups;
+    std::vector<uint32_t> dempty;
+    size_t o_voff = 0, o_lmsg = 0, o_leafrefs = 0, o_dempty = 0;
+    // SK_POC
+    size_t o_io = 0, o_oo = 0, o_salt = 0, o_out = 0;
+    uint64_t poc_max = 0;
+    uint32_t salt_len = 0;
+    // SK_HEADER
+    size_t o_hscr = 0;
+
+    Shape() = default;
+    Shape(const Shape&) = delete;
+    Shape& operator=(const Shape&) = delete;
+    ~Shape() {
+        if (ev) hipEventDestroy(ev);
+        if (owned && mem) hipFree(mem);
+    }
+    template <typename T>
+    void stage(size_t off, const T* p, size_t count) {
+        if (!count) return;
+        const uint8_t* b = (const uint8_t*)p;
+        uploads.emplace_back(off, std::vector<uint8_t>(b, b + count * sizeof(T)));
+    }
+    template <typename T>
+    T* at(size_t off) const { return (T*)(mem + off); }
+};
+
+constexpr size_t kMaxShapes = 32;
+constexpr size_t kMaxShapeBytes = (size_t)32 << 30;  // of the 288 GB of HBM
+
+}  // namespace
 
 struct gsv_ctx {
     int device = 0;
@@ -33,24 +130,14 @@ struct gsv_ctx {
     double total_ms[GSV_K_COUNT] = {0};
     long launches[GSV_K_COUNT] = {0};
     std::mutex tmu;
-    // chunk-root trie plans (per body length) and the device workspace of the *_dev paths
-    gsv::PlanCache plans;
-    uint8_t* work = nullptr;
-    size_t work_cap = 0;
     std::vector<hipEvent_t> open_ev;  // timer events opened by launch hooks
-    hipStream_t cur_stream = nullptr;
-    std::mutex wmu;                   // serializes users of `work`
-    uint8_t* nwork = nullptr;         // notary workspace (blob tables, chain-id buffers)
-    size_t nwork_cap = 0;
-    uint8_t* pwork = nullptr;         // Proof-of-Custody salted bodies (outlive `work` regrowth)
-    size_t pwork_cap = 0;
-    // ordering of `work` users on different streams: the last user's stream + an event after its work
-    hipStream_t work_st = nullptr;
-    hipEvent_t work_ev = nullptr;
-    // chunk-root body offsets cached on the device (re-uploaded only when they change)
-    uint64_t* coff = nullptr;
-    size_t coff_cap = 0;
-    std::vector<uint64_t> coff_key;
+    hipStream_t cur_stream = nullptr;  // stream of the shape run in progress (launch hooks)
+    bool cur_capture = false;          // that run is being captured into a graph: no timer events
+    // trie plans per body length, prepared shapes (most recently used first)
+    gsv::PlanCache plans;
+    std::list<std::unique_ptr<Shape>> shapes;
+    size_t shape_bytes = 0;
+    std::mutex smu;  // shapes, cur_stream / cur_capture
 };
 
 namespace {
@@ -63,6 +150,12 @@ int hip_err(hipError_t e) { return e == hipSuccess ? GSV_SUCCESS : GSV_E_HIP; }
         if (_e != hipSuccess) return GSV_E_HIP;    \
     } while (0)
 
+bool capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
+    return cs != hipStreamCaptureStatusNone;
+}
+
 hipEvent_t take_event(gsv_ctx* c) {
     if (!c->free_events.empty()) {
         hipEvent_t e = c->free_events.back();
@@ -74,14 +167,14 @@ hipEvent_t take_event(gsv_ctx* c) {
     return e;
 }
 
-// Brackets one launch with events on the launching stream when timing is on.
+// Brackets one launch with events on the launching stream when timing is on (never inside a capture).
 struct KTimer {
     gsv_ctx* c;
     int kid;
     hipStream_t st;
     hipEvent_t a = nullptr, b = nullptr;
     KTimer(gsv_ctx* c_, int kid_, hipStream_t st_) : c(c_), kid(kid_), st(st_) {
-        if (c->timing) {
+        if (c->timing && !capturing(st)) {
             std::lock_guard<std::mutex> g(c->tmu);
             a = take_event(c);
             b = take_event(c);
@@ -112,10 +205,10 @@ void drain_timing(gsv_ctx* c) {
     c->pending.clear();
 }
 
-// timer hooks for multi-launch paths (chunk root levels)
+// timer hooks for multi-launch paths (chunk-root levels, pairing stages)
 void hook_begin(void* p, int kid) {
     gsv_ctx* c = (gsv_ctx*)p;
-    if (!c->timing) return;
+    if (!c->timing || c->cur_capture) return;
     std::lock_guard<std::mutex> g(c->tmu);
     hipEvent_t a = take_event(c);
     hipEventRecord(a, c->cur_stream);
@@ -123,39 +216,13 @@ void hook_begin(void* p, int kid) {
 }
 void hook_end(void* p, int kid) {
     gsv_ctx* c = (gsv_ctx*)p;
-    if (!c->timing) return;
+    if (!c->timing || c->cur_capture) return;
     std::lock_guard<std::mutex> g(c->tmu);
     hipEvent_t a = c->open_ev.back();
     c->open_ev.pop_back();
     hipEvent_t b = take_event(c);
     hipEventRecord(b, c->cur_stream);
     c->pending.push_back({kid, a, b});
-}
-
-int work_reserve(gsv_ctx* c, size_t bytes) {
-    if (bytes <= c->work_cap) return GSV_SUCCESS;
-    size_t cap = c->work_cap ? c->work_cap : (size_t)64 << 20;
-    while (cap < bytes) cap *= 2;
-    if (c->work) {
-        hipDeviceSynchronize();
-        hipFree(c->work);
-        c->work = nullptr;
-        c->work_cap = 0;
-    }
-    if (hipMalloc(&c->work, cap) != hipSuccess) return GSV_E_NOMEM;
-    c->work_cap = cap;
-    return GSV_SUCCESS;
-}
-
-// `work` is shared by the *_dev paths of one context: a call on a stream other than the previous
-// user's waits (on the GPU) for that user's last enqueued work before touching it.
-void work_begin(gsv_ctx* c, hipStream_t st) {
-    if (c->work_st && c->work_st != st && c->work_ev) hipStreamWaitEvent(st, c->work_ev, 0);
-}
-void work_end(gsv_ctx* c, hipStream_t st) {
-    if (!c->work_ev) hipEventCreateWithFlags(&c->work_ev, hipEventDisableTiming);
-    if (c->work_ev) hipEventRecord(c->work_ev, st);
-    c->work_st = st;
 }
 
 int arena_reserve(gsv_ctx* c, size_t bytes) {
@@ -185,7 +252,146 @@ struct Carve {
         return p;
     }
 };
-size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// ------------------------------------------------------------------ prepared shapes
+// allocates (or, for a host-path shape, carves) the shape's memory and uploads its host tables
+int shape_materialize(Shape& s, size_t bytes, uint8_t* carve = nullptr) {
+    s.bytes = bytes;
+    if (carve) {
+        s.mem = carve;
+        s.owned = false;
+    } else if (hipMalloc(&s.mem, bytes ? bytes : 256) != hipSuccess) {
+        s.mem = nullptr;
+        return GSV_E_NOMEM;
+    }
+    for (auto& u : s.uploads) HIPCHK(hipMemcpy(s.mem + u.first, u.second.data(), u.second.size(), hipMemcpyHostToDevice));
+    s.uploads.clear();
+    s.uploads.shrink_to_fit();
+    if (s.owned) HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+    return GSV_SUCCESS;
+}
+
+Shape* shape_find(gsv_ctx* c, uint64_t kind, const std::vector<uint64_t>& key) {
+    for (auto it = c->shapes.begin(); it != c->shapes.end(); ++it) {
+        Shape* s = it->get();
+        if (s->kind == kind && s->key == key) {
+            if (it != c->shapes.begin()) c->shapes.splice(c->shapes.begin(), c->shapes, it);
+            return s;
+        }
+    }
+    return nullptr;
+}
+
+// inserts a materialized shape; drops least-recently-used shapes beyond the bounds (after their
+// queued work has drained — a graph captured from a dropped shape must not be replayed)
+void shape_insert(gsv_ctx* c, std::unique_ptr<Shape> s) {
+    c->shape_bytes += s->bytes;
+    c->shapes.push_front(std::move(s));
+    while (c->shapes.size() > 1 && (c->shapes.size() > kMaxShapes || c->shape_bytes > kMaxShapeBytes)) {
+        Shape* v = c->shapes.back().get();
+        if (v->ev) hipEventSynchronize(v->ev);
+        c->shape_bytes -= v->bytes;
+        c->shapes.pop_back();
+    }
+}
+
+// Runs a shape's launches on `st`.  Users of one shape on different streams are ordered on the GPU
+// (the workspace is the shape's); inside a stream capture no event is touched, and the caller orders
+// graph replays against other uses of the same shape.
+template <typename F>
+int shape_run(gsv_ctx* c, Shape& s, hipStream_t st, F&& body) {
+    bool cap = capturing(st);
+    if (!cap && s.ev && s.last && s.last != st) HIPCHK(hipStreamWaitEvent(st, s.ev, 0));
+    c->cur_stream = st;
+    c->cur_capture = cap;
+    int rc = body();
+    if (rc) return rc;
+    if (!cap && s.ev) {
+        HIPCHK(hipEventRecord(s.ev, st));
+        s.last = st;
+    }
+    return GSV_SUCCESS;
+}
+
+void key_push_bytes(std::vector<uint64_t>& key, const uint8_t* p, size_t n) {
+    key.push_back(n);
+    for (size_t i = 0; i < n; i += 8) {
+        uint64_t w = 0;
+        memcpy(&w, p + i, std::min<size_t>(8, n - i));
+        key.push_back(w);
+    }
+}
+
+// ------------------------------------------------------------------ chunk root launch description
+static const uint8_t EMPTY_ROOT[32] = {0x56, 0xe8, 0x1f, 0x17, 0x1b, 0xcc, 0x55, 0xa6, 0xff, 0x83, 0x45,
+                                       0xe6, 0x92, 0xc0, 0xf8, 0x6e, 0x5b, 0x48, 0xe0, 0x1b, 0x99, 0x6c,
+                                       0xad, 0xc0, 0x01, 0x62, 0x2f, 0xb5, 0xe3, 0x63, 0xb4, 0x21};
+constexpr uint64_t MAX_BODY = 1ull << 20;  // collationSizelimit (sharding/collation.go:45)
+constexpr uint64_t MAX_POC = 1ull << 26;   // salted bodies (Proof of Custody)
+constexpr uint64_t MAX_LIST = 1ull << 24;  // generic DeriveSha items per list
+
+std::vector<Run> runs_of(const std::vector<uint32_t>& idx) {
+    std::vector<Run> r;
+    size_t k = 0;
+    while (k < idx.size()) {
+        size_t e = k + 1;
+        while (e < idx.size() && idx[e] == idx[e - 1] + 1) e++;
+        r.push_back({idx[k], (uint32_t)k, (uint32_t)(e - k)});
+        k = e;
+    }
+    return r;
+}
+
+// bodies grouped by length (the trie shape depends only on N, chunk_root.h)
+int chunk_prepare(gsv_ctx* c, Shape& s, ChunkLaunch& cl, Layout& L, const uint64_t* start, const uint64_t* end,
+                  size_t n, uint64_t max_len) {
+    std::map<uint64_t, std::vector<uint32_t>> groups;
+    for (size_t i = 0; i < n; i++) {
+        if (end[i] < start[i] || end[i] - start[i] > max_len) return GSV_E_TOO_LARGE;
+        groups[end[i] - start[i]].push_back((uint32_t)i);
+    }
+    std::vector<uint64_t> offs;
+    offs.reserve(n);
+    for (auto& g : groups) {
+        if (g.first == 0) {  // empty trie -> emptyRoot (trie/trie.go:472-474)
+            cl.empty = g.second;
+            continue;
+        }
+        TrieGroup tg;
+        tg.plan = c->plans.get((uint32_t)g.first);
+        if (!tg.plan) return GSV_E_NOMEM;
+        tg.count = (uint32_t)g.second.size();
+        tg.koff = offs.size();
+        tg.direct = g.second.size() == n;
+        for (uint32_t i : g.second) offs.push_back(start[i]);
+        if (!tg.direct) {
+            tg.o_roots = L.add((size_t)tg.count * 32);
+            tg.runs = runs_of(g.second);
+        }
+        tg.o_scr = L.add(gsv::chunk_root_scratch_bytes(tg.plan.get(), tg.count));
+        cl.groups.push_back(std::move(tg));
+    }
+    cl.o_off = L.add(offs.size() * 8);
+    cl.o_empty = L.add(32);
+    s.stage(cl.o_off, offs.data(), offs.size());
+    s.stage(cl.o_empty, EMPTY_ROOT, 32);
+    return GSV_SUCCESS;
+}
+
+int chunk_run(gsv_ctx* c, const Shape& s, const ChunkLaunch& cl, const uint8_t* d_bodies, uint8_t* d_roots,
+              hipStream_t st) {
+    for (const TrieGroup& g : cl.groups) {
+        uint8_t* d_gr = g.direct ? d_roots : s.at<uint8_t>(g.o_roots);
+        HIPCHK(gsv::launch_chunk_root_plan(g.plan.get(), d_bodies, s.at<uint64_t>(cl.o_off) + g.koff, g.count,
+                                           s.at<uint8_t>(g.o_scr), d_gr, st, hook_begin, hook_end, c));
+        for (const Run& r : g.runs)
+            HIPCHK(hipMemcpyAsync(d_roots + (size_t)r.dst * 32, d_gr + (size_t)r.from * 32, (size_t)r.count * 32,
+                                  hipMemcpyDeviceToDevice, st));
+    }
+    for (uint32_t i : cl.empty)
+        HIPCHK(hipMemcpyAsync(d_roots + (size_t)i * 32, s.at<uint8_t>(cl.o_empty), 32, hipMemcpyDeviceToDevice, st));
+    return GSV_SUCCESS;
+}
 
 }  // namespace
 
@@ -208,6 +414,7 @@ const char* gsv_error_string(int err) {
         case GSV_E_NO_DEVICE: return "no HIP device";
         case GSV_E_TOO_LARGE: return "input exceeds the reference size limit";
         case GSV_E_RCCL: return "RCCL error";
+        case GSV_E_NOT_PREPARED: return "batch shape not prepared (call the matching gsv_*_prepare first)";
         default: return "unknown error";
     }
 }
@@ -245,15 +452,11 @@ int gsv_ctx_create(int device, gsv_ctx** out) {
 void gsv_ctx_destroy(gsv_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
+    hipDeviceSynchronize();  // every stream's work on the context's shapes has drained
     drain_timing(c);
     for (auto e : c->free_events) hipEventDestroy(e);
+    c->shapes.clear();
     if (c->arena) hipFree(c->arena);
-    if (c->work) hipFree(c->work);
-    if (c->nwork) hipFree(c->nwork);
-    if (c->pwork) hipFree(c->pwork);
-    if (c->coff) hipFree(c->coff);
-    if (c->work_ev) hipEventDestroy(c->work_ev);
     if (c->gtab) hipFree(c->gtab);
     hipStreamDestroy(c->stream);
     delete c;
@@ -283,6 +486,14 @@ int gsv_ctx_reset_timing(gsv_ctx* c) {
     return GSV_SUCCESS;
 }
 
+int gsv_ctx_prepared_shapes(gsv_ctx* c, size_t* count, size_t* device_bytes) {
+    if (!c) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->smu);
+    if (count) *count = c->shapes.size();
+    if (device_bytes) *device_bytes = c->shape_bytes;
+    return GSV_SUCCESS;
+}
+
 // ------------------------------------------------------------------ Keccak-256
 int gsv_keccak256_batch_dev(gsv_ctx* c, const uint8_t* d_data, const uint64_t* d_off, size_t n,
                             uint8_t* d_out32, void* stream) {
@@ -296,6 +507,9 @@ int gsv_keccak256_batch(gsv_ctx* c, const uint8_t* data, const uint64_t* off, si
                         uint8_t* out32) {
     if (!c || (n && (!off || !out32)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
+    for (size_t i = 0; i < n; i++)  // the kernel trusts off[i] <= off[i+1]
+        if (off[i + 1] < off[i]) return GSV_E_INVALID_ARG;
+    if (off[n] > off[0] && !data) return GSV_E_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     size_t bytes = off[n] - off[0];
@@ -350,6 +564,45 @@ int gsv_ecrecover_batch(gsv_ctx* c, const uint8_t* msg32, const uint8_t* sig65, 
     if (pub65_out) HIPCHK(hipMemcpyAsync(pub65_out, d_pub, n * 65, hipMemcpyDeviceToHost, c->stream));
     if (addr20_out) HIPCHK(hipMemcpyAsync(addr20_out, d_addr, n * 20, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ ecrecover precompile (contracts.go:78-101)
+int gsv_ecrecover_precompile_batch_dev(gsv_ctx* c, const uint8_t* d_in128, size_t n, uint8_t* d_out32, uint8_t* d_ok,
+                                       void* stream) {
+    if (!c || (n && (!d_in128 || !d_out32 || !d_ok)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    KTimer t(c, GSV_K_ECRECOVER, st);
+    return hip_err(gsv::launch_ecrecover_precompile(d_in128, (uint32_t)n, c->gtab, d_out32, d_ok, st));
+}
+
+int gsv_ecrecover_precompile_batch(gsv_ctx* c, const uint8_t* in, const uint64_t* off, size_t n, uint8_t* out32,
+                                   uint8_t* ok) {
+    if (!c || (n && (!off || !out32 || !ok)) || n > 0xFFFFFFFFull) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    for (size_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i]) return GSV_E_INVALID_ARG;
+    if (off[n] > off[0] && !in) return GSV_E_INVALID_ARG;
+    // common.RightPadBytes(input, 128); only input[0:128] is read (contracts.go:81-90)
+    std::vector<uint8_t> pad(n * 128, 0);
+    for (size_t i = 0; i < n; i++) {
+        size_t len = std::min<uint64_t>(off[i + 1] - off[i], 128);
+        if (len) memcpy(&pad[i * 128], in + off[i], len);
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    int rc = arena_reserve(c, al(n * 128) + al(n * 32) + al(n));
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_in = cv.take<uint8_t>(n * 128);
+    uint8_t* d_out = cv.take<uint8_t>(n * 32);
+    uint8_t* d_ok = cv.take<uint8_t>(n);
+    HIPCHK(hipMemcpyAsync(d_in, pad.data(), n * 128, hipMemcpyHostToDevice, c->stream));
+    rc = gsv_ecrecover_precompile_batch_dev(c, d_in, n, d_out, d_ok, c->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out32, d_out, n * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(ok, d_ok, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return GSV_SUCCESS;
 }
@@ -425,92 +678,395 @@ int gsv_synth_sign(gsv_ctx* c, uint64_t seed, size_t n, uint8_t* msg32, uint8_t*
     return GSV_SUCCESS;
 }
 
-// ------------------------------------------------------------------ chunk root
-static const uint8_t EMPTY_ROOT[32] = {0x56, 0xe8, 0x1f, 0x17, 0x1b, 0xcc, 0x55, 0xa6, 0xff, 0x83, 0x45,
-                                       0xe6, 0x92, 0xc0, 0xf8, 0x6e, 0x5b, 0x48, 0xe0, 0x1b, 0x99, 0x6c,
-                                       0xad, 0xc0, 0x01, 0x62, 0x2f, 0xb5, 0xe3, 0x63, 0xb4, 0x21};
-static const uint64_t MAX_BODY = 1ull << 20;  // collationSizelimit (sharding/collation.go:45)
+}  // extern "C"
 
-// Body i = d_bodies[start[i] .. end[i]); roots to d_roots (device) via workspace `work`.
-static int chunk_root_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* start,
-                               const uint64_t* end, size_t n, uint8_t* d_roots, hipStream_t st,
-                               uint64_t max_len = MAX_BODY) {
-    // group bodies by length (the trie shape depends only on N)
+// ================================================================== shape builders per entry point
+namespace {
+
+// ---- chunk root: key = body offsets
+std::vector<uint64_t> chunk_key(const uint64_t* h_off, size_t n) {
+    std::vector<uint64_t> k(h_off, h_off + n + 1);
+    return k;
+}
+int chunk_shape(gsv_ctx* c, Shape& s, const uint64_t* start, const uint64_t* end, size_t n, Layout& L) {
+    s.kind = SK_CHUNK;
+    return chunk_prepare(c, s, s.chunk, L, start, end, n, MAX_BODY);
+}
+
+// ---- BN254 pairing: check c = in[off[c] .. off[c+1]); a length that is not a multiple of 192 is
+// errBadPairingInput (core/vm/contracts.go:336-338) and contributes no pairs.
+// Final exponentiation layout: one lane per check is a ~10^4-product dependent chain; when the batch
+// gives the SIMDs fewer than one such wave each, three lanes per check share its exponentiations by
+// u (a third of the chain).  GSV_BN_FINAL3 = 0/1 forces the choice (A/B timing).
+bool bn_final3(size_t nchecks, int cus) {
+    if (const char* e = getenv("GSV_BN_FINAL3")) return atoi(e) != 0;
+    return nchecks < (size_t)std::max(cus, 1) * 4 * 64;
+}
+// Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
+// lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
+// and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
+// batches split a check over more lanes (k = 2, 1).  GSV_BN_PAIRS_PER_LANE forces k (A/B timing).
+uint32_t bn_pairs_per_lane(size_t np, int cus) {
+    if (const char* e = getenv("GSV_BN_PAIRS_PER_LANE")) {
+        int k = atoi(e);
+        if (k >= 1) return (uint32_t)k;
+    }
+    const size_t waves = 1;
+    size_t target = (size_t)std::max(cus, 1) * 4 * 64 * waves;
+    for (uint32_t k = 4; k > 1; k >>= 1)
+        if ((np + k - 1) / k >= target) return k;
+    return 1;
+}
+int device_cus(int device) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
+    return cus;
+}
+// key: the offsets plus the A/B overrides of the layout choice (tools/pairing_sweep.py)
+std::vector<uint64_t> pairing_key(const uint64_t* h_off, size_t n) {
+    const char* k = getenv("GSV_BN_PAIRS_PER_LANE");
+    const char* f = getenv("GSV_BN_FINAL3");
+    std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0};
+    key.insert(key.end(), h_off, h_off + n + 1);
+    return key;
+}
+int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L) {
+    s.kind = SK_PAIRING;
+    int cus = device_cus(c->device);
+    std::vector<uint8_t> bad_len(n, 0);
+    size_t np = 0, maxk = 0;
+    for (size_t k = 0; k < n; k++) {
+        if (off[k + 1] < off[k]) return GSV_E_INVALID_ARG;
+        uint64_t len = off[k + 1] - off[k];
+        if (len % 192) bad_len[k] = 1;
+        else {
+            np += len / 192;
+            maxk = std::max<size_t>(maxk, len / 192);
+        }
+    }
+    if (np > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
+    // slot-major order: slot k holds the k-th pair of every check that has more than k pairs
+    std::vector<uint64_t> per_slot(maxk + 1, 0), slot_base(maxk + 1, 0), fill(maxk + 1, 0);
+    for (size_t k = 0; k < n; k++)
+        if (!bad_len[k]) per_slot[(off[k + 1] - off[k]) / 192]++;  // histogram of pair counts
+    {
+        uint64_t more = 0, acc = 0;  // checks with > k pairs, from the top
+        std::vector<uint64_t> gt(maxk + 1, 0);
+        for (size_t k = maxk + 1; k-- > 0;) {
+            gt[k] = more;
+            more += per_slot[k];
+        }
+        for (size_t k = 0; k < maxk; k++) {
+            slot_base[k] = acc;
+            acc += gt[k];
+        }
+    }
+    std::vector<uint64_t> pair_src(np);
+    std::vector<uint32_t> pidx(np), check_first(n + 1);
+    size_t q = 0;
+    for (size_t k = 0; k < n; k++) {
+        check_first[k] = (uint32_t)q;
+        if (bad_len[k]) continue;
+        size_t slot = 0;
+        for (uint64_t o = off[k]; o < off[k + 1]; o += 192, slot++) {
+            uint64_t j = slot_base[slot] + fill[slot]++;
+            pair_src[j] = o;
+            pidx[q++] = (uint32_t)j;
+        }
+    }
+    check_first[n] = (uint32_t)q;
+    uint32_t kpl = bn_pairs_per_lane(np, cus);
+    std::vector<uint32_t> check_lane(n + 1), lane_first;
+    lane_first.reserve(n + np / kpl + 2);
+    for (size_t k = 0; k < n; k++) {
+        check_lane[k] = (uint32_t)lane_first.size();
+        uint32_t b = check_first[k], e = check_first[k + 1];
+        lane_first.push_back(b);  // a check without pairs still gets one (empty) lane
+        for (uint32_t p = b + kpl; p < e; p += kpl) lane_first.push_back(p);
+    }
+    check_lane[n] = (uint32_t)lane_first.size();
+    lane_first.push_back((uint32_t)q);
+    s.np = np;
+    s.nl = lane_first.size() - 1;
+    s.nchecks = n;
+    s.final3 = bn_final3(n, cus);
+    s.o_src = L.add(np * 8 + 8);
+    s.o_pidx = L.add(np * 4 + 4);
+    s.o_lfirst = L.add((s.nl + 1) * 4);
+    s.o_clane = L.add((n + 1) * 4);
+    s.o_cbad = L.add(n);
+    s.o_pstat = L.add(np + 1);
+    s.o_pts = L.add(np * 48 * 4 + 4);
+    s.o_rs = L.add(np * 64 * 4 + 4);
+    s.o_lstat = L.add(s.nl + 1);
+    s.o_fv = L.add(s.nl * 96 * 4 + 4);
+    s.stage(s.o_src, pair_src.data(), np);
+    s.stage(s.o_pidx, pidx.data(), np);
+    s.stage(s.o_lfirst, lane_first.data(), lane_first.size());
+    s.stage(s.o_clane, check_lane.data(), n + 1);
+    s.stage(s.o_cbad, bad_len.data(), n);
+    return GSV_SUCCESS;
+}
+int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verdict, hipStream_t st) {
+    return hip_err(gsv::launch_bn256_pairing(
+        d_in, s.at<uint64_t>(s.o_src), (uint32_t)s.np, s.at<uint32_t>(s.o_lfirst), s.at<uint32_t>(s.o_pidx),
+        (uint32_t)s.nl, s.at<uint32_t>(s.o_clane), s.at<uint8_t>(s.o_cbad), (uint32_t)s.nchecks,
+        s.at<uint8_t>(s.o_pstat), s.at<uint32_t>(s.o_pts), s.at<uint32_t>(s.o_rs), s.at<uint8_t>(s.o_lstat),
+        s.at<uint32_t>(s.o_fv), d_verdict, s.final3, st, hook_begin, hook_end, c));
+}
+
+// ---- notary: key = chain id, signer, max_txs, body offsets
+std::vector<uint64_t> notary_key(const uint64_t* h_off, size_t n, const uint8_t* cid, size_t cidlen, int signer,
+                                 uint32_t max_txs) {
+    std::vector<uint64_t> k{(uint64_t)signer, max_txs};
+    key_push_bytes(k, cid, cidlen);
+    k.insert(k.end(), h_off, h_off + n + 1);
+    return k;
+}
+int notary_shape(gsv_ctx* c, Shape& s, const uint64_t* start, const uint64_t* end, size_t n, const uint8_t* cid,
+                 size_t cidlen, int signer_kind, uint32_t max_txs, Layout& L) {
+    s.kind = SK_NOTARY;
+    if (cidlen > 64) return GSV_E_INVALID_ARG;
+    for (size_t i = 0; i < n; i++)
+        if (end[i] < start[i] || end[i] - start[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+    // chain-id buffers: 64-byte big-endian value and the sighash suffix rlp(chainId) || 0x80 0x80
+    uint8_t host[256] = {0};
+    if (cidlen) memcpy(host + 64 - cidlen, cid, cidlen);
+    size_t z = 0;
+    while (z < cidlen && cid[z] == 0) z++;
+    size_t cn = cidlen - z, sl = 0;
+    uint8_t* suf = host + 64;
+    if (cn == 1 && cid[z] < 0x80) suf[sl++] = cid[z];
+    else {
+        suf[sl++] = (uint8_t)(0x80 + cn);
+        if (cn) memcpy(suf + sl, cid + z, cn);
+        sl += cn;
+    }
+    suf[sl++] = 0x80;
+    suf[sl++] = 0x80;
+    std::vector<uint64_t> offs(n);
+    std::vector<uint32_t> lens(n);
+    for (size_t i = 0; i < n; i++) {
+        offs[i] = start[i];
+        lens[i] = (uint32_t)(end[i] - start[i]);
+    }
+    s.max_txs = max_txs;
+    s.signer_kind = signer_kind;
+    s.sfx_len = (uint32_t)sl;
+    s.o_cid = L.add(256);
+    s.o_noff = L.add(n * 8);
+    s.o_nlen = L.add(n * 4);
+    s.o_cnt = L.add(n * 4);
+    s.o_blobs = L.add((size_t)n * max_txs * gsv::blob_rec_bytes());
+    s.stage(s.o_cid, host, 256);
+    s.stage(s.o_noff, offs.data(), n);
+    s.stage(s.o_nlen, lens.data(), n);
+    return chunk_prepare(c, s, s.chunk, L, start, end, n, MAX_BODY);
+}
+int notary_run(gsv_ctx* c, const Shape& s, size_t n, const uint8_t* d_bodies, uint8_t* d_root, uint32_t* d_ntx,
+               uint8_t* d_bitmap, uint8_t* d_senders, uint8_t* d_status, hipStream_t st) {
+    size_t bm = (s.max_txs + 7) / 8;
+    uint32_t* d_cnt = d_ntx ? d_ntx : s.at<uint32_t>(s.o_cnt);
+    if (d_senders) HIPCHK(hipMemsetAsync(d_senders, 0, n * s.max_txs * 20, st));
+    if (d_status) HIPCHK(hipMemsetAsync(d_status, GSV_ST_BAD_RLP, n * s.max_txs, st));
+    hook_begin(c, GSV_K_NOTARY);
+    HIPCHK(gsv::launch_blob_index(d_bodies, s.at<uint64_t>(s.o_noff), s.at<uint32_t>(s.o_nlen), (uint32_t)n,
+                                  s.max_txs, s.at<void>(s.o_blobs), d_cnt, st));
+    HIPCHK(gsv::launch_notary_tx(d_bodies, s.at<uint64_t>(s.o_noff), s.at<void>(s.o_blobs), d_cnt, (uint32_t)n,
+                                 s.max_txs, s.at<uint8_t>(s.o_cid), s.at<uint8_t>(s.o_cid) + 64, s.sfx_len,
+                                 s.signer_kind, c->gtab, d_bitmap, (uint32_t)bm, d_senders, d_status, st));
+    hook_end(c, GSV_K_NOTARY);
+    return chunk_run(c, s, s.chunk, d_bodies, d_root, st);  // chunk roots of the same bodies
+}
+
+// ---- generic DeriveSha: key = list offsets and the items' value offsets
+std::vector<uint64_t> derive_key(const uint64_t* voff, const uint64_t* list_off, size_t n) {
+    std::vector<uint64_t> k(list_off, list_off + n + 1);
+    k.insert(k.end(), voff + list_off[0], voff + list_off[n] + 1);
+    return k;
+}
+// item k = d_vals[voff[k] .. voff[k+1]); list i = items [list_off[i], list_off[i+1])
+int derive_shape(gsv_ctx* c, Shape& s, const uint64_t* voff, const uint64_t* list_off, size_t n, Layout& L) {
+    s.kind = SK_DERIVE;
     std::map<uint64_t, std::vector<uint32_t>> groups;
     for (size_t i = 0; i < n; i++) {
-        if (end[i] < start[i] || end[i] - start[i] > max_len) return GSV_E_TOO_LARGE;
-        groups[end[i] - start[i]].push_back((uint32_t)i);
+        if (list_off[i + 1] < list_off[i]) return GSV_E_INVALID_ARG;
+        uint64_t N = list_off[i + 1] - list_off[i];
+        if (N > MAX_LIST) return GSV_E_TOO_LARGE;
+        groups[N].push_back((uint32_t)i);
     }
-    size_t need = 0;
-    std::vector<uint64_t> key;  // all groups' body offsets, in group order
-    key.reserve(n);
+    uint64_t total = list_off[n] - list_off[0];
+    for (uint64_t k = list_off[0]; k < list_off[n]; k++)
+        if (voff[k + 1] < voff[k] || voff[k + 1] - voff[k] >= (1ull << 32)) return GSV_E_INVALID_ARG;
+    // per-item leaf message buffers are placed by the kernel (k_derive_leaf): aligned bytes + 32 per item
+    uint64_t pos = ((voff[list_off[n]] - voff[list_off[0]] + 7) & ~7ull) + 32ull * total;
+    s.o_voff = L.add((total + 1) * 8);
+    s.o_lmsg = L.add(pos + 256);
+    s.o_leafrefs = L.add(total * 48);
+    s.o_dempty = L.add(32);
+    s.stage(s.o_voff, voff + list_off[0], total + 1);
+    s.stage(s.o_dempty, EMPTY_ROOT, 32);
     for (auto& g : groups) {
-        if (g.first == 0) continue;
-        gsv::TriePlan* pl = c->plans.get((uint32_t)g.first);
-        if (!pl) return GSV_E_NOMEM;
-        need += al(g.second.size() * 32) + al(gsv::chunk_root_scratch_bytes(pl, (uint32_t)g.second.size()));
-        for (uint32_t i : g.second) key.push_back(start[i]);
-    }
-    work_begin(c, st);
-    int rc = work_reserve(c, need + 4096);
-    if (rc) return rc;
-    // device copy of the offsets: uploaded only when they differ from the previous call's
-    if (key != c->coff_key) {
-        if (key.size() * 8 > c->coff_cap) {
-            if (c->coff) {
-                hipDeviceSynchronize();
-                hipFree(c->coff);
-                c->coff = nullptr;
-                c->coff_cap = 0;
-            }
-            size_t cap = (key.size() * 8 + 4095) & ~(size_t)4095;
-            if (hipMalloc(&c->coff, cap) != hipSuccess) return GSV_E_NOMEM;
-            c->coff_cap = cap;
-        }
-        if (!key.empty())  // pageable source: staged before return, so `key` may go out of scope
-            HIPCHK(hipMemcpyAsync(c->coff, key.data(), key.size() * 8, hipMemcpyHostToDevice, st));
-        c->coff_key = std::move(key);
-    }
-    Carve cv(c->work);
-    c->cur_stream = st;
-    size_t koff = 0;
-    for (auto& g : groups) {
-        const auto& idx = g.second;
-        if (g.first == 0) {  // empty trie -> emptyRoot (trie/trie.go:472-474)
-            for (uint32_t i : idx)
-                HIPCHK(hipMemcpyAsync(d_roots + (size_t)i * 32, EMPTY_ROOT, 32, hipMemcpyHostToDevice, st));
+        if (g.first == 0) {  // empty list -> emptyRoot (trie/trie.go:472-474)
+            s.dempty = g.second;
             continue;
         }
-        gsv::TriePlan* pl = c->plans.get((uint32_t)g.first);
-        bool direct = idx.size() == n;  // one group holding bodies 0..n-1 in order: roots in place
-        uint8_t* d_gr = direct ? d_roots : cv.take<uint8_t>(idx.size() * 32);
-        uint8_t* d_scr = cv.take<uint8_t>(gsv::chunk_root_scratch_bytes(pl, (uint32_t)idx.size()));
-        HIPCHK(gsv::launch_chunk_root_plan(pl, d_bodies, c->coff + koff, (uint32_t)idx.size(), d_scr, d_gr, st,
-                                           hook_begin, hook_end, c));
-        koff += idx.size();
-        if (direct) continue;
-        // scatter group roots to their positions (contiguous runs copied together)
-        size_t k = 0;
-        while (k < idx.size()) {
-            size_t e2 = k + 1;
-            while (e2 < idx.size() && idx[e2] == idx[e2 - 1] + 1) e2++;
-            HIPCHK(hipMemcpyAsync(d_roots + (size_t)idx[k] * 32, d_gr + k * 32, (e2 - k) * 32,
-                                  hipMemcpyDeviceToDevice, st));
-            k = e2;
-        }
+        TrieGroup tg;
+        tg.plan = c->plans.get((uint32_t)g.first, true);
+        if (!tg.plan) return GSV_E_NOMEM;
+        tg.count = (uint32_t)g.second.size();
+        std::vector<uint64_t> base(tg.count);
+        for (size_t k = 0; k < tg.count; k++) base[k] = list_off[g.second[k]] - list_off[0];
+        tg.o_base = L.add(tg.count * 8);
+        tg.o_roots = L.add((size_t)tg.count * 32);
+        tg.o_scr = L.add(gsv::derive_sha_scratch_bytes(tg.plan.get(), tg.count));
+        tg.runs = runs_of(g.second);
+        s.stage(tg.o_base, base.data(), base.size());
+        s.dgroups.push_back(std::move(tg));
     }
-    work_end(c, st);
     return GSV_SUCCESS;
+}
+int derive_run(gsv_ctx* c, const Shape& s, const uint8_t* d_vals, uint8_t* d_roots, hipStream_t st) {
+    for (const TrieGroup& g : s.dgroups) {
+        uint8_t* d_gr = s.at<uint8_t>(g.o_roots);
+        HIPCHK(gsv::launch_derive_sha_plan(g.plan.get(), g.count, d_vals, s.at<uint64_t>(s.o_voff),
+                                           s.at<uint64_t>(g.o_base), s.at<uint8_t>(s.o_lmsg),
+                                           s.at<uint8_t>(s.o_leafrefs), s.at<uint8_t>(g.o_scr), d_gr, st, hook_begin,
+                                           hook_end, c));
+        for (const Run& r : g.runs)
+            HIPCHK(hipMemcpyAsync(d_roots + (size_t)r.dst * 32, d_gr + (size_t)r.from * 32, (size_t)r.count * 32,
+                                  hipMemcpyDeviceToDevice, st));
+    }
+    for (uint32_t i : s.dempty)
+        HIPCHK(hipMemcpyAsync(d_roots + (size_t)i * 32, s.at<uint8_t>(s.o_dempty), 32, hipMemcpyDeviceToDevice, st));
+    return GSV_SUCCESS;
+}
+
+// ---- Proof of Custody: key = salt, body offsets
+std::vector<uint64_t> poc_key(const uint64_t* h_off, size_t n, const uint8_t* salt, size_t slen) {
+    std::vector<uint64_t> k;
+    key_push_bytes(k, salt, slen);
+    k.insert(k.end(), h_off, h_off + n + 1);
+    return k;
+}
+int poc_shape(gsv_ctx* c, Shape& s, const uint64_t* start, const uint64_t* end, size_t n, const uint8_t* salt,
+              size_t slen, Layout& L) {
+    s.kind = SK_POC;
+    std::vector<uint64_t> io(2 * n), oo(n), os(n), oe(n);
+    uint64_t pos = 0, mx = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (end[i] < start[i]) return GSV_E_INVALID_ARG;
+        uint64_t len = end[i] - start[i];
+        if (len > MAX_POC) return GSV_E_TOO_LARGE;
+        uint64_t N = len ? len * (slen + 1) : slen;
+        if (N > MAX_POC) return GSV_E_TOO_LARGE;
+        io[2 * i] = start[i];
+        io[2 * i + 1] = end[i];
+        oo[i] = os[i] = pos;
+        oe[i] = pos + N;
+        mx = N > mx ? N : mx;
+        pos = (oe[i] + 15) & ~15ull;
+    }
+    s.poc_max = mx;
+    s.salt_len = (uint32_t)slen;
+    s.o_io = L.add(2 * n * 8);
+    s.o_oo = L.add(n * 8);
+    s.o_salt = L.add(slen + 1);
+    s.o_out = L.add(pos + 16);
+    s.stage(s.o_io, io.data(), io.size());
+    s.stage(s.o_oo, oo.data(), oo.size());
+    s.stage(s.o_salt, salt, slen);
+    return chunk_prepare(c, s, s.chunk, L, os.data(), oe.data(), n, MAX_POC);
+}
+int poc_run(gsv_ctx* c, const Shape& s, size_t n, const uint8_t* d_bodies, uint8_t* d_poc, hipStream_t st) {
+    HIPCHK(gsv::launch_poc_expand(d_bodies, s.at<uint64_t>(s.o_io), s.at<uint64_t>(s.o_oo), (uint32_t)n, s.poc_max,
+                                  s.at<uint8_t>(s.o_salt), s.salt_len, s.at<uint8_t>(s.o_out), st));
+    return chunk_run(c, s, s.chunk, s.at<uint8_t>(s.o_out), d_poc, st);
+}
+
+// ---- collation headers: key = batch size
+int header_shape(gsv_ctx*, Shape& s, size_t n, Layout& L) {
+    s.kind = SK_HEADER;
+    s.o_hscr = L.add(gsv::header_scratch_bytes((uint32_t)n));
+    return GSV_SUCCESS;
+}
+
+// Prepare-or-find: returns the cached shape for (kind, key), building it with `build` on a miss.
+template <typename B>
+int shape_get(gsv_ctx* c, uint64_t kind, std::vector<uint64_t>&& key, B&& build, Shape** out) {
+    Shape* s = shape_find(c, kind, key);
+    if (!s) {
+        auto ns = std::make_unique<Shape>();
+        Layout L;
+        int rc = build(*ns, L);
+        if (rc) return rc;
+        rc = shape_materialize(*ns, L.n);
+        if (rc) return rc;
+        ns->kind = kind;
+        ns->key = std::move(key);
+        s = ns.get();
+        shape_insert(c, std::move(ns));
+    }
+    *out = s;
+    return GSV_SUCCESS;
+}
+
+// Host-path shape: built per call in the arena after `staged` bytes of inputs, run, synchronized.
+template <typename B>
+int shape_temp(gsv_ctx* c, size_t staged, B&& build, Shape& s) {
+    Layout L;
+    int rc = build(s, L);
+    if (rc) return rc;
+    rc = arena_reserve(c, staged + L.n);
+    if (rc) return rc;
+    return shape_materialize(s, L.n, c->arena + staged);
+}
+
+// bodies staged in HBM with 16-byte aligned starts (vector loads in the bottom-level kernel)
+uint64_t stage_offsets(const uint64_t* off, size_t n, std::vector<uint64_t>& st, std::vector<uint64_t>& en) {
+    st.resize(n);
+    en.resize(n);
+    uint64_t pos = 0;
+    for (size_t i = 0; i < n; i++) {
+        st[i] = pos;
+        en[i] = pos + (off[i + 1] - off[i]);
+        pos = (en[i] + 15) & ~15ull;
+    }
+    return pos;
+}
+int stage_bodies(gsv_ctx* c, uint8_t* d_b, const uint8_t* bodies, const uint64_t* off, size_t n,
+                 const std::vector<uint64_t>& st, const std::vector<uint64_t>& en) {
+    for (size_t i = 0; i < n; i++)
+        if (en[i] > st[i])
+            HIPCHK(hipMemcpyAsync(d_b + st[i], bodies + off[i], en[i] - st[i], hipMemcpyHostToDevice, c->stream));
+    return GSV_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------------ chunk root
+int gsv_chunk_root_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n) {
+    if (!c || (n && !h_off)) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->smu);
+    HIPCHK(hipSetDevice(c->device));
+    Shape* s;
+    return shape_get(c, SK_CHUNK, chunk_key(h_off, n),
+                     [&](Shape& ns, Layout& L) { return chunk_shape(c, ns, h_off, h_off + 1, n, L); }, &s);
 }
 
 int gsv_chunk_root_batch_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n,
                              uint8_t* d_root32_out, void* stream) {
     if (!c || (n && (!h_off || !d_root32_out || !d_bodies))) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
-    std::lock_guard<std::mutex> g(c->wmu);
+    std::lock_guard<std::mutex> g(c->smu);
+    Shape* s = shape_find(c, SK_CHUNK, chunk_key(h_off, n));
+    if (!s) return GSV_E_NOT_PREPARED;
     HIPCHK(hipSetDevice(c->device));
-    return chunk_root_dev_impl(c, d_bodies, h_off, h_off + 1, n, d_root32_out,
-                               stream ? (hipStream_t)stream : c->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return shape_run(c, *s, st, [&] { return chunk_run(c, *s, s->chunk, d_bodies, d_root32_out, st); });
 }
 
 int gsv_chunk_root_batch(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n, uint8_t* root32_out) {
@@ -518,29 +1074,24 @@ int gsv_chunk_root_batch(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off,
     if (n == 0) return GSV_SUCCESS;
     for (size_t i = 0; i < n; i++)
         if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+    if (off[n] > off[0] && !bodies) return GSV_E_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g2(c->smu);
     HIPCHK(hipSetDevice(c->device));
-    // stage bodies in HBM with 16-byte aligned starts (vector loads in the bottom-level kernel)
-    std::vector<uint64_t> st(n), en(n);
-    uint64_t pos = 0;
-    for (size_t i = 0; i < n; i++) {
-        st[i] = pos;
-        en[i] = pos + (off[i + 1] - off[i]);
-        pos = (en[i] + 15) & ~15ull;
-    }
-    int rc = arena_reserve(c, al(pos + 16) + al(n * 32));
+    std::vector<uint64_t> st, en;
+    uint64_t pos = stage_offsets(off, n, st, en);
+    size_t staged = al(pos + 16) + al(n * 32);
+    Shape s;
+    int rc = shape_temp(c, staged, [&](Shape& ns, Layout& L) { return chunk_shape(c, ns, st.data(), en.data(), n, L); },
+                        s);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_b = cv.take<uint8_t>(pos + 16);
     uint8_t* d_r = cv.take<uint8_t>(n * 32);
-    for (size_t i = 0; i < n; i++)
-        if (en[i] > st[i])
-            HIPCHK(hipMemcpyAsync(d_b + st[i], bodies + off[i], en[i] - st[i], hipMemcpyHostToDevice, c->stream));
-    {
-        std::lock_guard<std::mutex> g2(c->wmu);
-        rc = chunk_root_dev_impl(c, d_b, st.data(), en.data(), n, d_r, c->stream);
-        if (rc) return rc;
-    }
+    rc = stage_bodies(c, d_b, bodies, off, n, st, en);
+    if (rc) return rc;
+    rc = shape_run(c, s, c->stream, [&] { return chunk_run(c, s, s.chunk, d_b, d_r, c->stream); });
+    if (rc) return rc;
     HIPCHK(hipMemcpyAsync(root32_out, d_r, n * 32, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return GSV_SUCCESS;
@@ -552,7 +1103,6 @@ static int tx_sender_impl(gsv_ctx* c, const uint8_t* rlp, const uint64_t* off, s
                           size_t cidlen, int signer_kind, uint8_t* addr_out, uint8_t* status_out) {
     std::vector<uint8_t> hst(n), rr(n * 32), ss(n * 32), vb(n);
     std::vector<uint64_t> vv(n), plen(n);
-    std::vector<std::vector<uint8_t>> pres;
     unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     if (n < 4096) nt = 1;
     std::vector<std::vector<uint8_t>> tpre(nt);
@@ -632,148 +1182,23 @@ int gsv_tx_sender_batch(gsv_ctx* c, const uint8_t* rlp, const uint64_t* off, siz
     if (signer_kind < GSV_SIGNER_EIP155 || signer_kind > GSV_SIGNER_FRONTIER) return GSV_E_INVALID_ARG;
     if (chain_id_len && !chain_id) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
+    for (size_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i]) return GSV_E_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     return tx_sender_impl(c, rlp, off, n, chain_id, chain_id_len, signer_kind, addr20_out, status);
 }
 
 // ------------------------------------------------------------------ BN254 pairing check
-// Host tables for a batch: check c = in[off[c] .. off[c+1]); a length that is not a multiple of
-// 192 is errBadPairingInput (core/vm/contracts.go:336-338) and contributes no pairs.
-struct BnTables {
-    std::vector<uint64_t> pair_src;     // slot-major pair order
-    std::vector<uint32_t> check_first;  // check c's pairs: pidx[check_first[c] .. check_first[c+1])
-    std::vector<uint32_t> pidx;         // check-major position -> slot-major pair index
-    std::vector<uint32_t> lane_first;   // Miller lane l's pairs: pidx[lane_first[l] .. lane_first[l+1])
-    std::vector<uint32_t> check_lane;   // check c's Miller lanes: [check_lane[c], check_lane[c+1])
-    std::vector<uint8_t> bad_len;
-    bool final3 = false;                // final exponentiation on three cooperating lanes per check
-};
-// Final exponentiation layout: one lane per check is a ~10^4-product dependent chain; when the batch
-// gives the SIMDs fewer than one such wave each, three lanes per check share its exponentiations by
-// u (a third of the chain).  GSV_BN_FINAL3 = 0/1 forces the choice (A/B timing).
-static bool bn_final3(size_t nchecks, int cus) {
-    if (const char* e = getenv("GSV_BN_FINAL3")) return atoi(e) != 0;
-    return nchecks < (size_t)std::max(cus, 1) * 4 * 64;
-}
-// Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
-// lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
-// and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
-// batches split a check over more lanes (k = 2, 1).  GSV_BN_PAIRS_PER_LANE forces k (A/B timing).
-static uint32_t bn_pairs_per_lane(size_t np, int cus) {
-    if (const char* e = getenv("GSV_BN_PAIRS_PER_LANE")) {
-        int k = atoi(e);
-        if (k >= 1) return (uint32_t)k;
-    }
-    const size_t waves = 1;
-    size_t target = (size_t)std::max(cus, 1) * 4 * 64 * waves;
-    for (uint32_t k = 4; k > 1; k >>= 1)
-        if ((np + k - 1) / k >= target) return k;
-    return 1;
-}
-static int bn_tables(const uint64_t* off, size_t n, uint64_t base, int cus, BnTables& t) {
-    t.check_first.resize(n + 1);
-    t.bad_len.assign(n, 0);
-    size_t np = 0, maxk = 0;
-    for (size_t c = 0; c < n; c++) {
-        if (off[c + 1] < off[c]) return GSV_E_INVALID_ARG;
-        uint64_t len = off[c + 1] - off[c];
-        if (len % 192) t.bad_len[c] = 1;
-        else {
-            np += len / 192;
-            maxk = std::max<size_t>(maxk, len / 192);
-        }
-    }
-    if (np > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
-    // slot-major order: slot k holds the k-th pair of every check that has more than k pairs
-    std::vector<uint32_t> per_slot(maxk + 1, 0);
-    for (size_t c = 0; c < n; c++) {
-        if (t.bad_len[c]) continue;
-        per_slot[(off[c + 1] - off[c]) / 192]++;  // histogram of pair counts
-    }
-    std::vector<uint64_t> slot_base(maxk + 1, 0), fill(maxk + 1, 0);
-    {
-        uint64_t more = 0;  // checks with > k pairs, from the top
-        std::vector<uint64_t> gt(maxk + 1, 0);
-        for (size_t k = maxk + 1; k-- > 0;) {
-            gt[k] = more;
-            more += per_slot[k];
-        }
-        uint64_t acc = 0;
-        for (size_t k = 0; k < maxk; k++) {
-            slot_base[k] = acc;
-            acc += gt[k];
-        }
-    }
-    t.pair_src.resize(np);
-    t.pidx.resize(np);
-    size_t q = 0;
-    for (size_t c = 0; c < n; c++) {
-        t.check_first[c] = (uint32_t)q;
-        if (t.bad_len[c]) continue;
-        size_t k = 0;
-        for (uint64_t o = off[c]; o < off[c + 1]; o += 192, k++) {
-            uint64_t j = slot_base[k] + fill[k]++;
-            t.pair_src[j] = o - base;
-            t.pidx[q++] = (uint32_t)j;
-        }
-    }
-    t.check_first[n] = (uint32_t)q;
-    uint32_t k = bn_pairs_per_lane(np, cus);
-    t.check_lane.resize(n + 1);
-    t.lane_first.clear();
-    t.lane_first.reserve(n + np / k + 2);
-    for (size_t c = 0; c < n; c++) {
-        t.check_lane[c] = (uint32_t)t.lane_first.size();
-        uint32_t b = t.check_first[c], e = t.check_first[c + 1];
-        t.lane_first.push_back(b);  // a check without pairs still gets one (empty) lane
-        for (uint32_t p = b + k; p < e; p += k) t.lane_first.push_back(p);
-    }
-    t.check_lane[n] = (uint32_t)t.lane_first.size();
-    t.lane_first.push_back((uint32_t)q);
-    t.final3 = bn_final3(n, cus);
-    return GSV_SUCCESS;
-}
-static int device_cus(int device) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
-    return cus;
-}
-
-// enqueue the three pairing kernels; d_in already in HBM, tables from the host
-static int bn_run(gsv_ctx* c, const uint8_t* d_in, const BnTables& t, size_t n, uint8_t* d_verdict,
-                  hipStream_t st) {
-    size_t np = t.pair_src.size();
-    size_t nl = t.lane_first.size() - 1;
-    size_t need = al(np * 8 + 8) + al((nl + 1) * 4) + al((n + 1) * 4) + al(np * 4 + 4) + al(np + 1) +
-                  al(np * 48 * 4 + 4) + al(np * 64 * 4 + 4) + al(nl + 1) + al(nl * 96 * 4 + 4);
-    work_begin(c, st);
-    int rc = work_reserve(c, need + 4096);
-    if (rc) return rc;
-    Carve cv(c->work);
-    uint64_t* d_src = cv.take<uint64_t>(np * 8 + 8);
-    uint32_t* d_lfirst = cv.take<uint32_t>((nl + 1) * 4);
-    uint32_t* d_clane = cv.take<uint32_t>((n + 1) * 4);
-    uint32_t* d_pidx = cv.take<uint32_t>(np * 4 + 4);
-    uint8_t* d_pstat = cv.take<uint8_t>(np + 1);
-    uint32_t* d_pts = cv.take<uint32_t>(np * 48 * 4 + 4);
-    uint32_t* d_rs = cv.take<uint32_t>(np * 64 * 4 + 4);
-    uint8_t* d_lstat = cv.take<uint8_t>(nl + 1);
-    uint32_t* d_fv = cv.take<uint32_t>(nl * 96 * 4 + 4);
-    if (np) HIPCHK(hipMemcpyAsync(d_src, t.pair_src.data(), np * 8, hipMemcpyHostToDevice, st));
-    if (np) HIPCHK(hipMemcpyAsync(d_pidx, t.pidx.data(), np * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_lfirst, t.lane_first.data(), (nl + 1) * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_clane, t.check_lane.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
-    c->cur_stream = st;
-    HIPCHK(gsv::launch_bn256_pairing(d_in, d_src, (uint32_t)np, d_lfirst, d_pidx, (uint32_t)nl, d_clane, (uint32_t)n,
-                                     d_pstat, d_pts, d_rs, d_lstat, d_fv, d_verdict, t.final3, st, hook_begin,
-                                     hook_end, c));
-    // errBadPairingInput for ragged lengths overrides the kernel's verdict (those checks had no pairs)
-    static const uint8_t bad = GSV_PAIRING_BAD_INPUT;
-    for (size_t i = 0; i < n; i++)
-        if (t.bad_len[i]) HIPCHK(hipMemcpyAsync(d_verdict + i, &bad, 1, hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));  // host tables must outlive the async copies
-    return GSV_SUCCESS;
+int gsv_bn256_pairing_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n) {
+    if (!c || (n && !h_off)) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    if (n > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
+    std::lock_guard<std::mutex> g(c->smu);
+    HIPCHK(hipSetDevice(c->device));
+    Shape* s;
+    return shape_get(c, SK_PAIRING, pairing_key(h_off, n),
+                     [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, h_off, n, L); }, &s);
 }
 
 int gsv_bn256_pairing_check_batch_dev(gsv_ctx* c, const uint8_t* d_in, const uint64_t* h_off, size_t n,
@@ -781,37 +1206,38 @@ int gsv_bn256_pairing_check_batch_dev(gsv_ctx* c, const uint8_t* d_in, const uin
     if (!c || (n && (!h_off || !d_verdict))) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
     if (n > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
-    BnTables t;
-    int rc = bn_tables(h_off, n, 0, device_cus(c->device), t);
-    if (rc) return rc;
-    if (!t.pair_src.empty() && !d_in) return GSV_E_INVALID_ARG;
-    std::lock_guard<std::mutex> g(c->wmu);
+    std::lock_guard<std::mutex> g(c->smu);
+    Shape* s = shape_find(c, SK_PAIRING, pairing_key(h_off, n));
+    if (!s) return GSV_E_NOT_PREPARED;
+    if (s->np && !d_in) return GSV_E_INVALID_ARG;
     HIPCHK(hipSetDevice(c->device));
-    return bn_run(c, d_in, t, n, d_verdict, stream ? (hipStream_t)stream : c->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return shape_run(c, *s, st, [&] { return pairing_run(c, *s, d_in, d_verdict, st); });
 }
 
 int gsv_bn256_pairing_check_batch(gsv_ctx* c, const uint8_t* in, const uint64_t* off, size_t n, uint8_t* verdict) {
     if (!c || (n && (!off || !verdict))) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
     if (n > 0xFFFFFFFFull) return GSV_E_TOO_LARGE;
-    BnTables t;
-    int rc = bn_tables(off, n, off[0], device_cus(c->device), t);
-    if (rc) return rc;
-    if (!t.pair_src.empty() && !in) return GSV_E_INVALID_ARG;
+    for (size_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i]) return GSV_E_INVALID_ARG;
+    if (off[n] > off[0] && !in) return GSV_E_INVALID_ARG;
+    std::vector<uint64_t> rel(n + 1);
+    for (size_t i = 0; i <= n; i++) rel[i] = off[i] - off[0];
     std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g2(c->smu);
     HIPCHK(hipSetDevice(c->device));
     size_t bytes = off[n] - off[0];
-    rc = arena_reserve(c, al(bytes + 8) + al(n));
+    size_t staged = al(bytes + 8) + al(n);
+    Shape s;
+    int rc = shape_temp(c, staged, [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, rel.data(), n, L); }, s);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_in = cv.take<uint8_t>(bytes + 8);
     uint8_t* d_v = cv.take<uint8_t>(n);
     if (bytes) HIPCHK(hipMemcpyAsync(d_in, in + off[0], bytes, hipMemcpyHostToDevice, c->stream));
-    {
-        std::lock_guard<std::mutex> g2(c->wmu);
-        rc = bn_run(c, d_in, t, n, d_v, c->stream);
-        if (rc) return rc;
-    }
+    rc = shape_run(c, s, c->stream, [&] { return pairing_run(c, s, d_in, d_v, c->stream); });
+    if (rc) return rc;
     HIPCHK(hipMemcpyAsync(verdict, d_v, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return GSV_SUCCESS;
@@ -834,68 +1260,29 @@ int gsv_notary_synth_dev(gsv_ctx* c, uint64_t seed, uint32_t shard0, size_t n_sh
                                             d_exp_status, d_exp_sender, stream ? (hipStream_t)stream : c->stream));
 }
 
-static int notary_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* start, const uint64_t* end,
-                           size_t n, const uint8_t* cid, size_t cidlen, int signer_kind, uint32_t max_txs,
-                           uint8_t* d_root, uint32_t* d_ntx, uint8_t* d_bitmap, uint8_t* d_senders, uint8_t* d_status,
-                           hipStream_t st) {
-    if (cidlen > 64) return GSV_E_INVALID_ARG;
-    for (size_t i = 0; i < n; i++)
-        if (end[i] < start[i] || end[i] - start[i] > MAX_BODY) return GSV_E_TOO_LARGE;
-    work_begin(c, st);  // nwork / work of a previous call may still be in use on another stream
-    // chain-id buffers: 64-byte big-endian value and the sighash suffix rlp(chainId) || 0x80 0x80
-    uint8_t host[256] = {0};
-    memcpy(host + 64 - cidlen, cid, cidlen);
-    size_t z = 0;
-    while (z < cidlen && cid[z] == 0) z++;
-    size_t cn = cidlen - z, sl = 0;
-    uint8_t* suf = host + 64;
-    if (cn == 1 && cid[z] < 0x80) suf[sl++] = cid[z];
-    else {
-        suf[sl++] = (uint8_t)(0x80 + cn);
-        memcpy(suf + sl, cid + z, cn);
-        sl += cn;
-    }
-    suf[sl++] = 0x80;
-    suf[sl++] = 0x80;
-    std::vector<uint64_t> offs(n);
-    std::vector<uint32_t> lens(n);
-    for (size_t i = 0; i < n; i++) {
-        offs[i] = start[i];
-        lens[i] = (uint32_t)(end[i] - start[i]);
-    }
-    size_t bm = (max_txs + 7) / 8;
-    size_t need = al(256) + al(n * 8) + al(n * 4) + al(n * 4) + al((size_t)n * max_txs * gsv::blob_rec_bytes());
-    if (need > c->nwork_cap) {
-        size_t cap = std::max(need, (size_t)16 << 20);
-        if (c->nwork) {
-            hipDeviceSynchronize();
-            hipFree(c->nwork);
-            c->nwork = nullptr;
-            c->nwork_cap = 0;
-        }
-        if (hipMalloc(&c->nwork, cap) != hipSuccess) return GSV_E_NOMEM;
-        c->nwork_cap = cap;
-    }
-    Carve cv(c->nwork);
-    uint8_t* d_cid = cv.take<uint8_t>(256);
-    uint64_t* d_off = cv.take<uint64_t>(n * 8);
-    uint32_t* d_len = cv.take<uint32_t>(n * 4);
-    uint32_t* d_cnt = d_ntx ? d_ntx : cv.take<uint32_t>(n * 4);
-    void* d_blobs = cv.take<uint8_t>((size_t)n * max_txs * gsv::blob_rec_bytes());
-    HIPCHK(hipMemcpyAsync(d_cid, host, 256, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_off, offs.data(), n * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_len, lens.data(), n * 4, hipMemcpyHostToDevice, st));
-    if (d_senders) HIPCHK(hipMemsetAsync(d_senders, 0, (size_t)n * max_txs * 20, st));
-    if (d_status) HIPCHK(hipMemsetAsync(d_status, GSV_ST_BAD_RLP, (size_t)n * max_txs, st));
-    c->cur_stream = st;
-    hook_begin(c, GSV_K_NOTARY);
-    HIPCHK(gsv::launch_blob_index(d_bodies, d_off, d_len, (uint32_t)n, max_txs, d_blobs, d_cnt, st));
-    HIPCHK(gsv::launch_notary_tx(d_bodies, d_off, d_blobs, d_cnt, (uint32_t)n, max_txs, d_cid, d_cid + 64,
-                                 (uint32_t)sl, signer_kind, c->gtab, d_bitmap, (uint32_t)bm, d_senders, d_status,
-                                 st));
-    hook_end(c, GSV_K_NOTARY);
-    // chunk roots of the same bodies (own workspace)
-    return chunk_root_dev_impl(c, d_bodies, start, end, n, d_root, st);
+static int notary_args(const uint8_t* chain_id, size_t chain_id_len, int signer_kind, size_t n_shards,
+                       uint32_t max_txs) {
+    if ((chain_id_len && !chain_id) || chain_id_len > 64 || signer_kind < GSV_SIGNER_EIP155 ||
+        signer_kind > GSV_SIGNER_FRONTIER)
+        return GSV_E_INVALID_ARG;
+    if (n_shards > 65535 || max_txs == 0) return GSV_E_INVALID_ARG;
+    return GSV_SUCCESS;
+}
+
+int gsv_notary_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n_shards, const uint8_t* chain_id,
+                       size_t chain_id_len, int signer_kind, uint32_t max_txs) {
+    if (!c || (n_shards && !h_off)) return GSV_E_INVALID_ARG;
+    int rc = notary_args(chain_id, chain_id_len, signer_kind, n_shards, max_txs);
+    if (rc || n_shards == 0) return rc;
+    std::lock_guard<std::mutex> g(c->smu);
+    HIPCHK(hipSetDevice(c->device));
+    Shape* s;
+    return shape_get(c, SK_NOTARY, notary_key(h_off, n_shards, chain_id, chain_id_len, signer_kind, max_txs),
+                     [&](Shape& ns, Layout& L) {
+                         return notary_shape(c, ns, h_off, h_off + 1, n_shards, chain_id, chain_id_len, signer_kind,
+                                             max_txs, L);
+                     },
+                     &s);
 }
 
 int gsv_notary_validate_shards_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n_shards,
@@ -903,14 +1290,16 @@ int gsv_notary_validate_shards_dev(gsv_ctx* c, const uint8_t* d_bodies, const ui
                                    uint8_t* d_root32, uint32_t* d_ntx, uint8_t* d_bitmap, uint8_t* d_senders,
                                    uint8_t* d_status, void* stream) {
     if (!c || (n_shards && (!d_bodies || !h_off || !d_root32 || !d_bitmap))) return GSV_E_INVALID_ARG;
-    if ((chain_id_len && !chain_id) || signer_kind < GSV_SIGNER_EIP155 || signer_kind > GSV_SIGNER_FRONTIER)
-        return GSV_E_INVALID_ARG;
-    if (n_shards == 0) return GSV_SUCCESS;
-    if (n_shards > 65535 || max_txs == 0) return GSV_E_INVALID_ARG;
-    std::lock_guard<std::mutex> g(c->wmu);
+    int rc = notary_args(chain_id, chain_id_len, signer_kind, n_shards, max_txs);
+    if (rc || n_shards == 0) return rc;
+    std::lock_guard<std::mutex> g(c->smu);
+    Shape* s = shape_find(c, SK_NOTARY, notary_key(h_off, n_shards, chain_id, chain_id_len, signer_kind, max_txs));
+    if (!s) return GSV_E_NOT_PREPARED;
     HIPCHK(hipSetDevice(c->device));
-    return notary_dev_impl(c, d_bodies, h_off, h_off + 1, n_shards, chain_id, chain_id_len, signer_kind, max_txs,
-                           d_root32, d_ntx, d_bitmap, d_senders, d_status, stream ? (hipStream_t)stream : c->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return shape_run(c, *s, st, [&] {
+        return notary_run(c, *s, n_shards, d_bodies, d_root32, d_ntx, d_bitmap, d_senders, d_status, st);
+    });
 }
 
 int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n_shards,
@@ -918,41 +1307,39 @@ int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t
                                uint8_t* root32_out, uint32_t* ntx_out, uint8_t* valid_bitmap_out,
                                uint8_t* senders_out, uint8_t* status_out) {
     if (!c || (n_shards && (!bodies || !off || !root32_out || !ntx_out || !valid_bitmap_out))) return GSV_E_INVALID_ARG;
-    if ((chain_id_len && !chain_id) || signer_kind < GSV_SIGNER_EIP155 || signer_kind > GSV_SIGNER_FRONTIER)
-        return GSV_E_INVALID_ARG;
-    if (n_shards == 0) return GSV_SUCCESS;
-    if (n_shards > 65535 || max_txs == 0 || chain_id_len > 64) return GSV_E_INVALID_ARG;
+    int rc = notary_args(chain_id, chain_id_len, signer_kind, n_shards, max_txs);
+    if (rc || n_shards == 0) return rc;
     for (size_t i = 0; i < n_shards; i++)
         if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_BODY) return GSV_E_TOO_LARGE;
     std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g2(c->smu);
     HIPCHK(hipSetDevice(c->device));
-    std::vector<uint64_t> st(n_shards), en(n_shards);
-    uint64_t pos = 0;
-    for (size_t i = 0; i < n_shards; i++) {
-        st[i] = pos;
-        en[i] = pos + (off[i + 1] - off[i]);
-        pos = (en[i] + 15) & ~15ull;
-    }
+    std::vector<uint64_t> st, en;
+    uint64_t pos = stage_offsets(off, n_shards, st, en);
     size_t bm = (max_txs + 7) / 8, nt = n_shards * (size_t)max_txs;
-    int rc = arena_reserve(c, al(pos + 16) + al(n_shards * 32) + al(n_shards * 4) + al(n_shards * bm) +
-                                  al(nt * 20) + al(nt));
+    size_t staged = al(pos + 16) + al(n_shards * 32) + al(n_shards * 4) + al(n_shards * bm) + al(nt * 20) + al(nt);
+    Shape s;
+    rc = shape_temp(c, staged,
+                    [&](Shape& ns, Layout& L) {
+                        return notary_shape(c, ns, st.data(), en.data(), n_shards, chain_id, chain_id_len,
+                                            signer_kind, max_txs, L);
+                    },
+                    s);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_b = cv.take<uint8_t>(pos + 16);
     uint8_t* d_r = cv.take<uint8_t>(n_shards * 32);
     uint32_t* d_n = cv.take<uint32_t>(n_shards * 4);
     uint8_t* d_bm = cv.take<uint8_t>(n_shards * bm);
-    uint8_t* d_snd = senders_out ? cv.take<uint8_t>(nt * 20) : nullptr;
-    uint8_t* d_st = status_out ? cv.take<uint8_t>(nt) : nullptr;
-    for (size_t i = 0; i < n_shards; i++)
-        if (en[i] > st[i])
-            HIPCHK(hipMemcpyAsync(d_b + st[i], bodies + off[i], en[i] - st[i], hipMemcpyHostToDevice, c->stream));
-    {
-        std::lock_guard<std::mutex> g2(c->wmu);
-        rc = notary_dev_impl(c, d_b, st.data(), en.data(), n_shards, chain_id, chain_id_len, signer_kind, max_txs,
-                             d_r, d_n, d_bm, d_snd, d_st, c->stream);
-        if (rc) return rc;
-    }
+    uint8_t* d_snd = cv.take<uint8_t>(nt * 20);
+    uint8_t* d_st = cv.take<uint8_t>(nt);
+    rc = stage_bodies(c, d_b, bodies, off, n_shards, st, en);
+    if (rc) return rc;
+    rc = shape_run(c, s, c->stream, [&] {
+        return notary_run(c, s, n_shards, d_b, d_r, d_n, d_bm, senders_out ? d_snd : nullptr,
+                          status_out ? d_st : nullptr, c->stream);
+    });
+    if (rc) return rc;
     HIPCHK(hipMemcpyAsync(root32_out, d_r, n_shards * 32, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(ntx_out, d_n, n_shards * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(valid_bitmap_out, d_bm, n_shards * bm, hipMemcpyDeviceToHost, c->stream));
@@ -965,166 +1352,92 @@ int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t
 }
 
 // ------------------------------------------------------------------ DeriveSha over any DerivableList
-static const uint64_t MAX_LIST = 1ull << 24;
-
-// item k = d_vals[voff[k] .. voff[k+1]); list i = items [list_off[i], list_off[i+1])
-static int derive_sha_dev_impl(gsv_ctx* c, const uint8_t* d_vals, const uint64_t* voff, const uint64_t* list_off,
-                               size_t n, uint8_t* d_roots, hipStream_t st) {
-    std::map<uint64_t, std::vector<uint32_t>> groups;
-    for (size_t i = 0; i < n; i++) {
+static int derive_args(const uint64_t* voff, const uint64_t* list_off, size_t n) {
+    if (list_off[n] < list_off[0]) return GSV_E_INVALID_ARG;
+    for (size_t i = 0; i < n; i++)
         if (list_off[i + 1] < list_off[i]) return GSV_E_INVALID_ARG;
-        uint64_t N = list_off[i + 1] - list_off[i];
-        if (N > MAX_LIST) return GSV_E_TOO_LARGE;
-        groups[N].push_back((uint32_t)i);
-    }
-    uint64_t total = list_off[n] - list_off[0];
-    for (uint64_t k = list_off[0]; k < list_off[n]; k++)
-        if (voff[k + 1] < voff[k] || voff[k + 1] - voff[k] >= (1ull << 32)) return GSV_E_INVALID_ARG;
-    // per item: message buffer offset (8-aligned, value + 24 bytes of RLP headers) and ref slot
-    // per-item leaf message buffers are placed by the kernel (k_derive_leaf): aligned bytes + 32 per item
-    uint64_t pos = ((voff[list_off[n]] - voff[list_off[0]] + 7) & ~7ull) + 32ull * total;
-    size_t need = al((total + 1) * 8) + al(pos + 256) + al(total * 48);
-    for (auto& g : groups) {
-        if (g.first == 0) continue;
-        gsv::TriePlan* pl = c->plans.get((uint32_t)g.first, true);
-        if (!pl) return GSV_E_NOMEM;
-        need += al(g.second.size() * 8) + al(g.second.size() * 32) +
-                al(gsv::derive_sha_scratch_bytes(pl, (uint32_t)g.second.size()));
-    }
-    work_begin(c, st);
-    int rc = work_reserve(c, need + 4096);
-    if (rc) return rc;
-    Carve cv(c->work);
-    c->cur_stream = st;
-    // voff rebased to d_vals is what the caller gave; items indexed from list_off[0]
-    uint64_t* d_voff = cv.take<uint64_t>((total + 1) * 8);
-    uint8_t* d_lmsg = cv.take<uint8_t>(pos + 256);
-    uint8_t* d_leafrefs = cv.take<uint8_t>(total * 48);
-    HIPCHK(hipMemcpyAsync(d_voff, voff + list_off[0], (total + 1) * 8, hipMemcpyHostToDevice, st));
-    std::vector<std::vector<uint64_t>> host_base;
-    host_base.reserve(groups.size());
-    for (auto& g : groups) {
-        const auto& idx = g.second;
-        if (g.first == 0) {  // empty list -> emptyRoot (trie/trie.go:472-474)
-            for (uint32_t i : idx)
-                HIPCHK(hipMemcpyAsync(d_roots + (size_t)i * 32, EMPTY_ROOT, 32, hipMemcpyHostToDevice, st));
-            continue;
-        }
-        gsv::TriePlan* pl = c->plans.get((uint32_t)g.first, true);
-        uint64_t* d_base = cv.take<uint64_t>(idx.size() * 8);
-        uint8_t* d_gr = cv.take<uint8_t>(idx.size() * 32);
-        uint8_t* d_scr = cv.take<uint8_t>(gsv::derive_sha_scratch_bytes(pl, (uint32_t)idx.size()));
-        host_base.emplace_back(idx.size());
-        auto& hb = host_base.back();
-        for (size_t k = 0; k < idx.size(); k++) hb[k] = list_off[idx[k]] - list_off[0];
-        HIPCHK(hipMemcpyAsync(d_base, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(gsv::launch_derive_sha_plan(pl, (uint32_t)idx.size(), d_vals, d_voff, d_base, d_lmsg,
-                                           d_leafrefs, d_scr, d_gr, st, hook_begin, hook_end, c));
-        size_t k = 0;
-        while (k < idx.size()) {
-            size_t e2 = k + 1;
-            while (e2 < idx.size() && idx[e2] == idx[e2 - 1] + 1) e2++;
-            HIPCHK(hipMemcpyAsync(d_roots + (size_t)idx[k] * 32, d_gr + k * 32, (e2 - k) * 32,
-                                  hipMemcpyDeviceToDevice, st));
-            k = e2;
-        }
-    }
-    HIPCHK(hipStreamSynchronize(st));  // host staging must outlive the async copies
     return GSV_SUCCESS;
+}
+
+int gsv_derive_sha_prepare(gsv_ctx* c, const uint64_t* voff, const uint64_t* list_off, size_t n) {
+    if (!c || (n && (!voff || !list_off))) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    int rc = derive_args(voff, list_off, n);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->smu);
+    HIPCHK(hipSetDevice(c->device));
+    Shape* s;
+    return shape_get(c, SK_DERIVE, derive_key(voff, list_off, n),
+                     [&](Shape& ns, Layout& L) { return derive_shape(c, ns, voff, list_off, n, L); }, &s);
 }
 
 int gsv_derive_sha_batch_dev(gsv_ctx* c, const uint8_t* d_vals, const uint64_t* voff, const uint64_t* list_off,
                              size_t n, uint8_t* d_root32_out, void* stream) {
     if (!c || (n && (!voff || !list_off || !d_root32_out))) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
+    int rc = derive_args(voff, list_off, n);
+    if (rc) return rc;
     if (list_off[n] > list_off[0] && !d_vals) return GSV_E_INVALID_ARG;
-    std::lock_guard<std::mutex> g(c->wmu);
+    std::lock_guard<std::mutex> g(c->smu);
+    Shape* s = shape_find(c, SK_DERIVE, derive_key(voff, list_off, n));
+    if (!s) return GSV_E_NOT_PREPARED;
     HIPCHK(hipSetDevice(c->device));
-    return derive_sha_dev_impl(c, d_vals, voff, list_off, n, d_root32_out, stream ? (hipStream_t)stream : c->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return shape_run(c, *s, st, [&] { return derive_run(c, *s, d_vals, d_root32_out, st); });
 }
 
 int gsv_derive_sha_batch(gsv_ctx* c, const uint8_t* vals, const uint64_t* voff, const uint64_t* list_off, size_t n,
                          uint8_t* root32_out) {
     if (!c || (n && (!voff || !list_off || !root32_out))) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
-    if (list_off[n] < list_off[0]) return GSV_E_INVALID_ARG;
+    int rc = derive_args(voff, list_off, n);
+    if (rc) return rc;
     uint64_t v0 = voff[list_off[0]], v1 = voff[list_off[n]];
     if (v1 < v0 || (v1 > v0 && !vals)) return GSV_E_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g2(c->smu);
     HIPCHK(hipSetDevice(c->device));
     // stage the values (rebased so item list_off[0] starts at 0)
     std::vector<uint64_t> rv(list_off[n] + 1, 0);
     for (uint64_t k = list_off[0]; k <= list_off[n]; k++) rv[k] = voff[k] - v0;
-    int rc = arena_reserve(c, al(v1 - v0 + 16) + al(n * 32));
+    size_t staged = al(v1 - v0 + 16) + al(n * 32);
+    Shape s;
+    rc = shape_temp(c, staged, [&](Shape& ns, Layout& L) { return derive_shape(c, ns, rv.data(), list_off, n, L); },
+                    s);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_v = cv.take<uint8_t>(v1 - v0 + 16);
     uint8_t* d_r = cv.take<uint8_t>(n * 32);
     if (v1 > v0) HIPCHK(hipMemcpyAsync(d_v, vals + v0, v1 - v0, hipMemcpyHostToDevice, c->stream));
-    {
-        std::lock_guard<std::mutex> g2(c->wmu);
-        rc = derive_sha_dev_impl(c, d_v, rv.data(), list_off, n, d_r, c->stream);
-        if (rc) return rc;
-    }
+    rc = shape_run(c, s, c->stream, [&] { return derive_run(c, s, d_v, d_r, c->stream); });
+    if (rc) return rc;
     HIPCHK(hipMemcpyAsync(root32_out, d_r, n * 32, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return GSV_SUCCESS;
 }
 
 // ------------------------------------------------------------------ Proof of Custody
-static const uint64_t MAX_POC = 1ull << 26;
-
-static int poc_dev_impl(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* start, const uint64_t* end, size_t n,
-                        const uint8_t* salt, size_t slen, uint8_t* d_poc, hipStream_t st) {
-    work_begin(c, st);  // pwork of a previous call may still be read on another stream
-    std::vector<uint64_t> io(2 * n), oo(n), os(n), oe(n);
-    uint64_t pos = 0, mx = 0;
-    for (size_t i = 0; i < n; i++) {
-        if (end[i] < start[i]) return GSV_E_INVALID_ARG;
-        uint64_t L = end[i] - start[i];
-        if (L > MAX_POC) return GSV_E_TOO_LARGE;
-        uint64_t N = L ? L * (slen + 1) : slen;
-        if (N > MAX_POC) return GSV_E_TOO_LARGE;
-        io[2 * i] = start[i];
-        io[2 * i + 1] = end[i];
-        oo[i] = os[i] = pos;
-        oe[i] = pos + N;
-        mx = N > mx ? N : mx;
-        pos = (oe[i] + 15) & ~15ull;
-    }
-    size_t need = al(pos + 16) + al(2 * n * 8) + al(n * 8) + al(slen + 1);
-    if (need > c->pwork_cap) {
-        size_t cap = c->pwork_cap ? c->pwork_cap : (size_t)64 << 20;
-        while (cap < need) cap *= 2;
-        if (c->pwork) {
-            hipDeviceSynchronize();
-            hipFree(c->pwork);
-            c->pwork = nullptr;
-            c->pwork_cap = 0;
-        }
-        if (hipMalloc(&c->pwork, cap) != hipSuccess) return GSV_E_NOMEM;
-        c->pwork_cap = cap;
-    }
-    Carve cv(c->pwork);
-    uint8_t* d_out = cv.take<uint8_t>(pos + 16);
-    uint64_t* d_io = cv.take<uint64_t>(2 * n * 8);
-    uint64_t* d_oo = cv.take<uint64_t>(n * 8);
-    uint8_t* d_salt = cv.take<uint8_t>(slen + 1);
-    HIPCHK(hipMemcpyAsync(d_io, io.data(), 2 * n * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_oo, oo.data(), n * 8, hipMemcpyHostToDevice, st));
-    if (slen) HIPCHK(hipMemcpyAsync(d_salt, salt, slen, hipMemcpyHostToDevice, st));
-    HIPCHK(gsv::launch_poc_expand(d_bodies, d_io, d_oo, (uint32_t)n, mx, d_salt, (uint32_t)slen, d_out, st));
-    return chunk_root_dev_impl(c, d_out, os.data(), oe.data(), n, d_poc, st, MAX_POC);
+int gsv_collation_poc_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n, const uint8_t* salt, size_t salt_len) {
+    if (!c || (n && !h_off) || (salt_len && !salt)) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    std::lock_guard<std::mutex> g(c->smu);
+    HIPCHK(hipSetDevice(c->device));
+    Shape* s;
+    return shape_get(c, SK_POC, poc_key(h_off, n, salt, salt_len),
+                     [&](Shape& ns, Layout& L) { return poc_shape(c, ns, h_off, h_off + 1, n, salt, salt_len, L); },
+                     &s);
 }
 
 int gsv_collation_poc_batch_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n,
                                 const uint8_t* salt, size_t salt_len, uint8_t* d_poc32_out, void* stream) {
     if (!c || (n && (!h_off || !d_poc32_out)) || (salt_len && !salt)) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
-    std::lock_guard<std::mutex> g(c->wmu);
+    std::lock_guard<std::mutex> g(c->smu);
+    Shape* s = shape_find(c, SK_POC, poc_key(h_off, n, salt, salt_len));
+    if (!s) return GSV_E_NOT_PREPARED;
     HIPCHK(hipSetDevice(c->device));
-    return poc_dev_impl(c, d_bodies, h_off, h_off + 1, n, salt, salt_len, d_poc32_out,
-                        stream ? (hipStream_t)stream : c->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return shape_run(c, *s, st, [&] { return poc_run(c, *s, n, d_bodies, d_poc32_out, st); });
 }
 
 int gsv_collation_poc_batch(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n, const uint8_t* salt,
@@ -1133,34 +1446,44 @@ int gsv_collation_poc_batch(gsv_ctx* c, const uint8_t* bodies, const uint64_t* o
     if (n == 0) return GSV_SUCCESS;
     for (size_t i = 0; i < n; i++)
         if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_POC) return GSV_E_TOO_LARGE;
+    if (off[n] > off[0] && !bodies) return GSV_E_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g2(c->smu);
     HIPCHK(hipSetDevice(c->device));
-    std::vector<uint64_t> st(n), en(n);
-    uint64_t pos = 0;
-    for (size_t i = 0; i < n; i++) {
-        st[i] = pos;
-        en[i] = pos + (off[i + 1] - off[i]);
-        pos = (en[i] + 15) & ~15ull;
-    }
-    int rc = arena_reserve(c, al(pos + 16) + al(n * 32));
+    std::vector<uint64_t> st, en;
+    uint64_t pos = stage_offsets(off, n, st, en);
+    size_t staged = al(pos + 16) + al(n * 32);
+    Shape s;
+    int rc = shape_temp(c, staged,
+                        [&](Shape& ns, Layout& L) {
+                            return poc_shape(c, ns, st.data(), en.data(), n, salt, salt_len, L);
+                        },
+                        s);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_b = cv.take<uint8_t>(pos + 16);
     uint8_t* d_r = cv.take<uint8_t>(n * 32);
-    for (size_t i = 0; i < n; i++)
-        if (en[i] > st[i])
-            HIPCHK(hipMemcpyAsync(d_b + st[i], bodies + off[i], en[i] - st[i], hipMemcpyHostToDevice, c->stream));
-    {
-        std::lock_guard<std::mutex> g2(c->wmu);
-        rc = poc_dev_impl(c, d_b, st.data(), en.data(), n, salt, salt_len, d_r, c->stream);
-        if (rc) return rc;
-    }
+    rc = stage_bodies(c, d_b, bodies, off, n, st, en);
+    if (rc) return rc;
+    rc = shape_run(c, s, c->stream, [&] { return poc_run(c, s, n, d_b, d_r, c->stream); });
+    if (rc) return rc;
     HIPCHK(hipMemcpyAsync(poc32_out, d_r, n * 32, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return GSV_SUCCESS;
 }
 
 // ------------------------------------------------------------------ collation header + proposer signature
+int gsv_collation_header_prepare(gsv_ctx* c, size_t n) {
+    if (!c) return GSV_E_INVALID_ARG;
+    if (n == 0) return GSV_SUCCESS;
+    if (n > (1u << 30)) return GSV_E_TOO_LARGE;
+    std::lock_guard<std::mutex> g(c->smu);
+    HIPCHK(hipSetDevice(c->device));
+    Shape* s;
+    return shape_get(c, SK_HEADER, std::vector<uint64_t>{n},
+                     [&](Shape& ns, Layout& L) { return header_shape(c, ns, n, L); }, &s);
+}
+
 int gsv_collation_header_verify_batch_dev(gsv_ctx* c, const uint8_t* d_sid, const uint8_t* d_root,
                                           const uint8_t* d_per, const uint8_t* d_prop, const uint8_t* d_sig,
                                           const uint8_t* d_nil, size_t n, uint8_t* d_hash, uint8_t* d_signer,
@@ -1168,19 +1491,16 @@ int gsv_collation_header_verify_batch_dev(gsv_ctx* c, const uint8_t* d_sid, cons
     if (!c || (n && (!d_sid || !d_root || !d_per || !d_prop || !d_sig || !d_st))) return GSV_E_INVALID_ARG;
     if (n == 0) return GSV_SUCCESS;
     if (n > (1u << 30)) return GSV_E_TOO_LARGE;
-    std::lock_guard<std::mutex> g(c->wmu);
+    std::lock_guard<std::mutex> g(c->smu);
+    Shape* s = shape_find(c, SK_HEADER, std::vector<uint64_t>{n});
+    if (!s) return GSV_E_NOT_PREPARED;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    work_begin(c, st);
-    int rc = work_reserve(c, al(gsv::header_scratch_bytes((uint32_t)n)));
-    if (rc) return rc;
-    {
+    return shape_run(c, *s, st, [&] {
         KTimer t(c, GSV_K_HEADER, st);
-        HIPCHK(gsv::launch_header_verify(d_sid, d_root, d_per, d_prop, d_sig, d_nil, (uint32_t)n, c->gtab, c->work,
-                                         d_hash, d_signer, d_st, st));
-    }
-    work_end(c, st);
-    return GSV_SUCCESS;
+        return hip_err(gsv::launch_header_verify(d_sid, d_root, d_per, d_prop, d_sig, d_nil, (uint32_t)n, c->gtab,
+                                                 s->at<uint8_t>(s->o_hscr), d_hash, d_signer, d_st, st));
+    });
 }
 
 int gsv_collation_header_verify_batch(gsv_ctx* c, const uint8_t* shard_id32, const uint8_t* chunk_root32,

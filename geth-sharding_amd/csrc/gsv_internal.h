@@ -14,6 +14,8 @@ hipError_t launch_ecrecover(const uint8_t* msg32, const uint8_t* sig65, uint32_t
 hipError_t launch_sender(const uint8_t* sighash32, const uint8_t* r32, const uint8_t* s32,
                          const uint64_t* v, const uint8_t* vbig, uint32_t n, int homestead,
                          const uint4* gtab, uint8_t* addr20, uint8_t* status, hipStream_t st);
+hipError_t launch_ecrecover_precompile(const uint8_t* in128, uint32_t n, const uint4* gtab, uint8_t* out32,
+                                       uint8_t* ok, hipStream_t st);
 hipError_t launch_synth_sign(uint64_t seed, uint32_t n, const uint4* gtab, uint8_t* msg32,
                              uint8_t* sig65, uint8_t* pub65, uint8_t* addr20, hipStream_t st);
 
@@ -49,15 +51,16 @@ hipError_t launch_header_verify(const uint8_t* d_sid32, const uint8_t* d_root32,
 // bn256.hip: pairs in slot-major order (the j-th pairs of all checks contiguous): pair_src[p] = byte
 // offset of pair p in d_in.  A check's pairs are split into Miller lanes of <= k pairs each: lane l
 // runs the multi-Miller loop over pidx[lane_first[l] .. lane_first[l+1]), check c owns lanes
-// [check_lane[c], check_lane[c+1]).  Workspaces: pstat[npairs], pts[48][npairs], rs[64][npairs],
-// lstat[nlanes], fv[96][nlanes] words.  final3: the final exponentiation runs on three cooperating
-// lanes per check (small batches)
+// [check_lane[c], check_lane[c+1]); cbad[c] != 0 marks a ragged input length (no pairs, verdict
+// BAD_INPUT).  Workspaces: pstat[npairs], pts[48][npairs], rs[64][npairs], lstat[nlanes],
+// fv[96][nlanes] words.  final3: the final exponentiation runs on three cooperating lanes per check
+// (small batches)
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
-                                const uint32_t* d_check_lane, uint32_t nchecks, uint8_t* d_pstat, uint32_t* d_pts,
-                                uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv, uint8_t* d_verdict, bool final3,
-                                hipStream_t st, void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
-                                void* tctx);
+                                const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
+                                uint8_t* d_pstat, uint32_t* d_pts, uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv,
+                                uint8_t* d_verdict, bool final3, hipStream_t st, void (*timer_begin)(void*, int),
+                                void (*timer_end)(void*, int), void* tctx);
 
 hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st);
 

@@ -210,10 +210,20 @@ def _chunk_root_batch(self, bodies) -> np.ndarray:
     return out
 
 
-def _chunk_root_batch_dev(self, bodies_t, h_off, roots_t, stream=None):
-    """bodies_t: torch uint8 CUDA tensor holding all bodies; h_off: numpy uint64 offsets (n+1)."""
+def _chunk_root_prepare(self, h_off):
+    """gsv_chunk_root_prepare: trie plans, device offset table and workspace for these offsets."""
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    check(_lib.load().gsv_chunk_root_prepare(self._h, _ptr(h_off), h_off.shape[0] - 1))
+
+
+def _chunk_root_batch_dev(self, bodies_t, h_off, roots_t, stream=None, prepare=True):
+    """bodies_t: torch uint8 CUDA tensor holding all bodies; h_off: numpy uint64 offsets (n+1).
+    prepare=False skips the (idempotent, host-side) gsv_chunk_root_prepare: the call then only
+    enqueues (graph-capturable) and raises GSV_E_NOT_PREPARED if the offsets were never prepared."""
     h_off = np.ascontiguousarray(h_off, np.uint64)
     n = h_off.shape[0] - 1
+    if prepare:
+        _chunk_root_prepare(self, h_off)
     sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
     check(_lib.load().gsv_chunk_root_batch_dev(self._h, ctypes.c_void_p(bodies_t.data_ptr()), _ptr(h_off), n,
                                                ctypes.c_void_p(roots_t.data_ptr()), sp))
@@ -231,10 +241,17 @@ def _pairing_check_batch(self, inputs) -> np.ndarray:
     return out
 
 
-def _pairing_check_batch_dev(self, in_t, h_off, verdict_t, stream=None):
+def _pairing_prepare(self, h_off):
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    check(_lib.load().gsv_bn256_pairing_prepare(self._h, _ptr(h_off), h_off.shape[0] - 1))
+
+
+def _pairing_check_batch_dev(self, in_t, h_off, verdict_t, stream=None, prepare=True):
     """in_t: torch uint8 CUDA tensor with all checks; h_off: numpy uint64 offsets (n+1)."""
     h_off = np.ascontiguousarray(h_off, np.uint64)
     n = h_off.shape[0] - 1
+    if prepare:
+        _pairing_prepare(self, h_off)
     sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
     check(_lib.load().gsv_bn256_pairing_check_batch_dev(self._h, ctypes.c_void_p(in_t.data_ptr()), _ptr(h_off),
                                                         n, ctypes.c_void_p(verdict_t.data_ptr()), sp))
@@ -276,11 +293,21 @@ def _notary_validate_shards(self, bodies, chain_id: int = 1, signer_kind: int = 
     return roots, ntx, bitmap, senders, status
 
 
+def _notary_prepare(self, h_off, chain_id: int = 1, signer_kind: int = _lib.SIGNER_EIP155, max_txs: int = 8192):
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    cid = _be(chain_id)
+    cbuf = np.frombuffer(cid + b"\0", np.uint8)
+    check(_lib.load().gsv_notary_prepare(self._h, _ptr(h_off), h_off.shape[0] - 1, _ptr(cbuf), len(cid),
+                                         int(signer_kind), int(max_txs)))
+
+
 def _notary_validate_shards_dev(self, bodies_t, h_off, roots_t, ntx_t, bitmap_t, senders_t=None, status_t=None,
                                 chain_id: int = 1, signer_kind: int = _lib.SIGNER_EIP155, max_txs: int = 8192,
-                                stream=None):
+                                stream=None, prepare=True):
     h_off = np.ascontiguousarray(h_off, np.uint64)
     n = h_off.shape[0] - 1
+    if prepare:
+        _notary_prepare(self, h_off, chain_id, signer_kind, max_txs)
     cid = _be(chain_id)
     cbuf = np.frombuffer(cid + b"\0", np.uint8)
     sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
@@ -297,6 +324,9 @@ def _notary_synth_dev(self, seed, shard0, n_shards, txs_per_shard, bodies_t, exp
                                            _tptr(exp_sender_t), sp))
 
 
+Context.notary_prepare = _notary_prepare
+Context.chunk_root_prepare = _chunk_root_prepare
+Context.pairing_prepare = _pairing_prepare
 Context.notary_validate_shards = _notary_validate_shards
 Context.notary_validate_shards_dev = _notary_validate_shards_dev
 Context.notary_synth_dev = _notary_synth_dev
@@ -322,11 +352,19 @@ def _derive_sha_batch(self, lists) -> np.ndarray:
     return out
 
 
-def _derive_sha_batch_dev(self, vals_t, voff, list_off, roots_t, stream=None):
+def _derive_sha_prepare(self, voff, list_off):
+    voff = np.ascontiguousarray(voff, np.uint64)
+    list_off = np.ascontiguousarray(list_off, np.uint64)
+    check(_lib.load().gsv_derive_sha_prepare(self._h, _ptr(voff), _ptr(list_off), list_off.shape[0] - 1))
+
+
+def _derive_sha_batch_dev(self, vals_t, voff, list_off, roots_t, stream=None, prepare=True):
     """vals_t: torch uint8 CUDA tensor of all item bytes; voff (items+1) / list_off (lists+1): numpy uint64."""
     voff = np.ascontiguousarray(voff, np.uint64)
     list_off = np.ascontiguousarray(list_off, np.uint64)
     n = list_off.shape[0] - 1
+    if prepare:
+        _derive_sha_prepare(self, voff, list_off)
     sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
     check(_lib.load().gsv_derive_sha_batch_dev(self._h, _tptr(vals_t), _ptr(voff), _ptr(list_off), n,
                                                _tptr(roots_t), sp))
@@ -344,9 +382,17 @@ def _collation_poc_batch(self, bodies, salt: bytes) -> np.ndarray:
     return out
 
 
-def _collation_poc_batch_dev(self, bodies_t, h_off, salt: bytes, out_t, stream=None):
+def _collation_poc_prepare(self, h_off, salt: bytes):
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    sb = np.frombuffer(bytes(salt) + b"\0", np.uint8)
+    check(_lib.load().gsv_collation_poc_prepare(self._h, _ptr(h_off), h_off.shape[0] - 1, _ptr(sb), len(salt)))
+
+
+def _collation_poc_batch_dev(self, bodies_t, h_off, salt: bytes, out_t, stream=None, prepare=True):
     h_off = np.ascontiguousarray(h_off, np.uint64)
     n = h_off.shape[0] - 1
+    if prepare:
+        _collation_poc_prepare(self, h_off, salt)
     sb = np.frombuffer(bytes(salt) + b"\0", np.uint8)
     sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
     check(_lib.load().gsv_collation_poc_batch_dev(self._h, _tptr(bodies_t), _ptr(h_off), n, _ptr(sb), len(salt),
@@ -375,8 +421,10 @@ def _collation_header_verify_batch(self, shard_id32, chunk_root32, period32, pro
 
 
 def _collation_header_verify_batch_dev(self, sid_t, root_t, per_t, prop_t, sig_t, st_t, nil_t=None, hash_t=None,
-                                       signer_t=None, stream=None):
+                                       signer_t=None, stream=None, prepare=True):
     n = sid_t.shape[0]
+    if prepare:
+        check(_lib.load().gsv_collation_header_prepare(self._h, n))
     sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
     check(_lib.load().gsv_collation_header_verify_batch_dev(self._h, _tptr(sid_t), _tptr(root_t), _tptr(per_t),
                                                             _tptr(prop_t), _tptr(sig_t), _tptr(nil_t), n,
@@ -389,3 +437,37 @@ Context.derive_sha_batch_dev = _derive_sha_batch_dev
 Context.collation_poc_batch = _collation_poc_batch
 Context.collation_poc_batch_dev = _collation_poc_batch_dev
 Context.collation_header_verify_batch = _collation_header_verify_batch
+Context.derive_sha_prepare = _derive_sha_prepare
+Context.collation_poc_prepare = _collation_poc_prepare
+
+
+def _ecrecover_precompile_batch(self, inputs):
+    """The ecrecover precompile's Run over many inputs (core/vm/contracts.go:78-101): returns
+    (out32 (n,32), ok (n,)); ok[i] == 0 where the reference returns (nil, nil)."""
+    n = len(inputs)
+    out = np.zeros((n, 32), np.uint8)
+    ok = np.zeros(n, np.uint8)
+    if n == 0:
+        return out, ok
+    flat, off = _pack(inputs)
+    check(_lib.load().gsv_ecrecover_precompile_batch(self._h, _ptr(flat), _ptr(off), n, _ptr(out), _ptr(ok)))
+    return out, ok
+
+
+def _ecrecover_precompile_batch_dev(self, in_t, out_t, ok_t, stream=None):
+    """in_t: torch uint8 CUDA tensor (n, 128) of right-padded precompile inputs."""
+    n = in_t.shape[0]
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_ecrecover_precompile_batch_dev(self._h, _tptr(in_t), n, _tptr(out_t), _tptr(ok_t), sp))
+
+
+def _prepared_shapes(self):
+    cnt = ctypes.c_size_t()
+    nb = ctypes.c_size_t()
+    check(_lib.load().gsv_ctx_prepared_shapes(self._h, ctypes.byref(cnt), ctypes.byref(nb)))
+    return cnt.value, nb.value
+
+
+Context.ecrecover_precompile_batch = _ecrecover_precompile_batch
+Context.ecrecover_precompile_batch_dev = _ecrecover_precompile_batch_dev
+Context.prepared_shapes = _prepared_shapes

@@ -46,6 +46,15 @@ K_NOTARY = 8
 K_DERIVE_LEAF = 9
 K_HEADER = 10
 
+# API errors (negative return values)
+E_INVALID_ARG = -1
+E_HIP = -2
+E_NOMEM = -3
+E_NO_DEVICE = -4
+E_TOO_LARGE = -5
+E_RCCL = -6
+E_NOT_PREPARED = -7
+
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -89,6 +98,15 @@ SIGNATURES = [
     ("gsv_collation_header_verify_batch", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     ("gsv_collation_header_verify_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp,
                                                              _vp]),
+    ("gsv_ctx_prepared_shapes", ctypes.c_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
+    ("gsv_ecrecover_precompile_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    ("gsv_ecrecover_precompile_batch_dev", ctypes.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
+    ("gsv_chunk_root_prepare", ctypes.c_int, [_vp, _vp, _sz]),
+    ("gsv_bn256_pairing_prepare", ctypes.c_int, [_vp, _vp, _sz]),
+    ("gsv_notary_prepare", ctypes.c_int, [_vp, _vp, _sz, _vp, _sz, ctypes.c_int, ctypes.c_uint32]),
+    ("gsv_derive_sha_prepare", ctypes.c_int, [_vp, _vp, _vp, _sz]),
+    ("gsv_collation_poc_prepare", ctypes.c_int, [_vp, _vp, _sz, _vp, _sz]),
+    ("gsv_collation_header_prepare", ctypes.c_int, [_vp, _sz]),
 ]
 
 _lib = None
@@ -96,7 +114,11 @@ _lock = threading.Lock()
 
 
 class GsvError(RuntimeError):
-    """A negative GSV_E_* return value from the library."""
+    """A negative GSV_E_* return value from the library (`code`)."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 def load():
@@ -128,4 +150,4 @@ def load():
 def check(rc: int):
     if rc != 0:
         msg = load().gsv_error_string(rc).decode()
-        raise GsvError(f"libgsv error {rc}: {msg}")
+        raise GsvError(f"libgsv error {rc}: {msg}", rc)

@@ -6,6 +6,7 @@
     SigToPub(hash, sig)         crypto/signature_cgo.go:36-44 (returns the 65-byte key here)
     EcrecoverBatch(...)         batch form used by the notary / tx pool hooks
     Keccak256Batch(msgs)        batch form
+    Ecrecover precompile        core/vm/contracts.go:70-101 (EcrecoverPrecompile.Run / RunBatch)
 
 Errors mirror crypto/secp256k1/secp256.go:54-62 and are raised as exceptions.
 """
@@ -77,3 +78,30 @@ def EcrecoverBatch(hashes, sigs, want_pub=True, want_addr=False, ctx=None):
 def PubkeyToAddress(pub65: bytes) -> bytes:
     """crypto/crypto.go:194-197: Keccak256(pub[1:])[12:]."""
     return Keccak256(bytes(pub65)[1:])[12:]
+
+
+def ValidateSignatureValues(v: int, r: int, s: int, homestead: bool) -> bool:
+    """crypto/crypto.go:181-192 (host-side predicate; the kernels apply the same rule per lane)."""
+    n = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+    if r < 1 or s < 1:
+        return False
+    if homestead and s > n // 2:
+        return False
+    return r < n and s < n and v in (0, 1)
+
+
+class EcrecoverPrecompile:
+    """PrecompiledContract{RequiredGas, Run} for address 0x01 (core/vm/contracts.go:70-101)."""
+
+    ECRECOVER_GAS = 3000  # params.EcrecoverGas
+
+    def RequiredGas(self, input: bytes) -> int:
+        return self.ECRECOVER_GAS
+
+    def Run(self, input: bytes, ctx=None):
+        """32-byte left-padded signer address, or None where the reference returns (nil, nil)."""
+        out, ok = self.RunBatch([bytes(input)], ctx)
+        return bytes(out[0]) if ok[0] else None
+
+    def RunBatch(self, inputs, ctx=None):
+        return (ctx or default_context()).ecrecover_precompile_batch(list(inputs))

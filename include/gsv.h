@@ -28,12 +28,23 @@
  *                                 proposer signature made by SMCClient.Sign (sharding/mainchain/
  *                                 smc_client.go:245-248, signed at sharding/proposer/proposer.go:83)
  *
+ *   gsv_ecrecover_precompile_batch <- the ecrecover precompile's Run (core/vm/contracts.go:78-101)
+ *
  * Conventions
  *   - Return value: GSV_SUCCESS (0) or a negative GSV_E_* API/HIP error. A bad ITEM never fails
  *     the batch: it gets a per-item status code (GSV_ST_*) mirroring the reference's errors.
  *   - Host-pointer entry points copy inputs to HBM, run, and copy results back (synchronous).
  *   - *_dev entry points take DEVICE pointers already resident in HBM and a hipStream_t passed
- *     as void*; they enqueue and return (asynchronous, graph-capturable: no allocation or sync).
+ *     as void*; they only enqueue: they never allocate device memory and never synchronize, so a
+ *     *_dev call can be captured into a HIP graph (hipStreamBeginCapture).
+ *   - *_dev entry points whose launch depends on host-side arguments (offset tables, chain id,
+ *     salt, batch size: chunk root, pairing, notary, DeriveSha, POC, headers) need that exact
+ *     argument set PREPARED first by the matching gsv_*_prepare call, which builds the trie plans
+ *     and lane tables, uploads them to HBM and sizes the workspace (it may allocate and
+ *     synchronize).  Unprepared -> GSV_E_NOT_PREPARED, nothing enqueued.  A context keeps its 32
+ *     most recently used prepared shapes (<= 32 GiB); a HIP graph captured from a shape must not
+ *     be replayed after that shape was dropped, and the caller orders graph replays against other
+ *     uses of the same shape (non-captured calls on different streams are ordered by the library).
  *   - One gsv_ctx per device; a context is safe to use from several threads on distinct streams
  *     for the *_dev calls; host-pointer calls serialize on the context's internal stream.
  */
@@ -57,6 +68,7 @@ extern "C" {
 #define GSV_E_NO_DEVICE (-4)
 #define GSV_E_TOO_LARGE (-5) /* e.g. collation body > 2^20 (sharding/collation.go:45) */
 #define GSV_E_RCCL (-6)
+#define GSV_E_NOT_PREPARED (-7) /* *_dev call whose host-side arguments were not gsv_*_prepare'd */
 
 /* ---- per-item status codes (mirror the reference's error values) ---- */
 #define GSV_ST_OK 0
@@ -111,6 +123,8 @@ int gsv_ctx_set_timing(gsv_ctx *ctx, int enable);
 /* total milliseconds and launch count accumulated for kernel `kid` since the last reset */
 int gsv_ctx_kernel_time(gsv_ctx *ctx, int kid, double *total_ms, long *launches);
 int gsv_ctx_reset_timing(gsv_ctx *ctx);
+/* prepared *_dev shapes currently cached and their device bytes */
+int gsv_ctx_prepared_shapes(gsv_ctx *ctx, size_t *count, size_t *device_bytes);
 
 /* ---- Keccak-256 (A10) ----
  * Message i is data[off[i] .. off[i+1]); out32[32*i .. +32) = Keccak256(message i). */
@@ -129,6 +143,18 @@ int gsv_ecrecover_batch(gsv_ctx *ctx, const uint8_t *msg32, const uint8_t *sig65
 int gsv_ecrecover_batch_dev(gsv_ctx *ctx, const uint8_t *d_msg32, const uint8_t *d_sig65, size_t n,
                             uint8_t *d_pub65_out, uint8_t *d_addr20_out, uint8_t *d_status,
                             void *stream);
+
+/* ---- the ecrecover precompile (core/vm/contracts.go:78-101) ----
+ * Input i = in[off[i] .. off[i+1]) = hash(32) || v(32) || r(32) || s(32), right-padded with zeros to
+ * 128 bytes (longer inputs: only the first 128 bytes are read).  ok[i] = 1 and out32[i] =
+ * LeftPadBytes(Keccak256(pub[1:])[12:], 32) on success; ok[i] = 0 and out32[i] zero where the
+ * reference returns (nil, nil): input[32:63] not all zero, ValidateSignatureValues(v - 27, r, s,
+ * homestead = false) false (crypto/crypto.go:181-192), or recovery failing. */
+int gsv_ecrecover_precompile_batch(gsv_ctx *ctx, const uint8_t *in, const uint64_t *off, size_t n,
+                                   uint8_t *out32, uint8_t *ok);
+/* Device-resident form over padded records: d_in128 = n x 128 bytes in HBM. */
+int gsv_ecrecover_precompile_batch_dev(gsv_ctx *ctx, const uint8_t *d_in128, size_t n, uint8_t *d_out32,
+                                       uint8_t *d_ok, void *stream);
 
 /* ---- recoverPlain (A4): sighash + (R, S, V) -> sender address ----
  * r32/s32: n x 32 B big-endian; v: per-item V already reduced by the signer
@@ -150,6 +176,9 @@ int gsv_tx_sender_batch(gsv_ctx *ctx, const uint8_t *rlp, const uint64_t *off, s
  * root32_out[i] = DeriveSha(Chunks(body i)); an empty body gives emptyRoot. */
 int gsv_chunk_root_batch(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off, size_t n,
                          uint8_t *root32_out);
+/* Prepares gsv_chunk_root_batch_dev for exactly these host offsets h_off[0..n] (trie plans per body
+ * length, device offset table, workspace). */
+int gsv_chunk_root_prepare(gsv_ctx *ctx, const uint64_t *h_off, size_t n);
 int gsv_chunk_root_batch_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off, size_t n,
                              uint8_t *d_root32_out, void *stream);
 
@@ -159,7 +188,9 @@ int gsv_chunk_root_batch_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64
 int gsv_bn256_pairing_check_batch(gsv_ctx *ctx, const uint8_t *in, const uint64_t *off, size_t n,
                                   uint8_t *verdict);
 /* Device-resident form: d_in in HBM, h_off on the host (n+1 offsets into d_in), d_verdict in HBM.
- * Enqueues on `stream` (NULL = the context stream); returns after the launches are queued. */
+ * Enqueues on `stream` (NULL = the context stream); returns after the launches are queued.
+ * gsv_bn256_pairing_prepare builds the lane tables for exactly these offsets. */
+int gsv_bn256_pairing_prepare(gsv_ctx *ctx, const uint64_t *h_off, size_t n);
 int gsv_bn256_pairing_check_batch_dev(gsv_ctx *ctx, const uint8_t *d_in, const uint64_t *h_off, size_t n,
                                       uint8_t *d_verdict, void *stream);
 
@@ -193,7 +224,10 @@ int gsv_notary_validate_shards(gsv_ctx *ctx, const uint8_t *bodies, const uint64
                                const uint8_t *chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
                                uint8_t *root32_out, uint32_t *ntx_out, uint8_t *valid_bitmap_out,
                                uint8_t *senders_out, uint8_t *status_out);
-/* Device-resident form: d_bodies/outputs in HBM, h_off on the host; enqueues on `stream`. */
+/* Device-resident form: d_bodies/outputs in HBM, h_off on the host; enqueues on `stream`.
+ * gsv_notary_prepare prepares it for exactly (h_off, chain id, signer_kind, max_txs). */
+int gsv_notary_prepare(gsv_ctx *ctx, const uint64_t *h_off, size_t n_shards, const uint8_t *chain_id,
+                       size_t chain_id_len, int signer_kind, uint32_t max_txs);
 int gsv_notary_validate_shards_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off, size_t n_shards,
                                    const uint8_t *chain_id, size_t chain_id_len, int signer_kind,
                                    uint32_t max_txs, uint8_t *d_root32, uint32_t *d_ntx, uint8_t *d_bitmap,
@@ -214,7 +248,9 @@ int gsv_notary_synth_dev(gsv_ctx *ctx, uint64_t seed, uint32_t shard0, size_t n_
 int gsv_derive_sha_batch(gsv_ctx *ctx, const uint8_t *vals, const uint64_t *voff, const uint64_t *list_off,
                          size_t n_lists, uint8_t *root32_out);
 /* Device-resident form: d_vals in HBM; voff / list_off on the host (offsets into d_vals / item
- * indices); d_root32_out in HBM; enqueues on `stream` (NULL = the context stream). */
+ * indices); d_root32_out in HBM; enqueues on `stream` (NULL = the context stream).
+ * gsv_derive_sha_prepare prepares it for exactly (voff, list_off). */
+int gsv_derive_sha_prepare(gsv_ctx *ctx, const uint64_t *voff, const uint64_t *list_off, size_t n_lists);
 int gsv_derive_sha_batch_dev(gsv_ctx *ctx, const uint8_t *d_vals, const uint64_t *voff, const uint64_t *list_off,
                              size_t n_lists, uint8_t *d_root32_out, void *stream);
 
@@ -223,6 +259,7 @@ int gsv_derive_sha_batch_dev(gsv_ctx *ctx, const uint8_t *d_vals, const uint64_t
  * (salt alone for an empty body).  The salted body may hold up to 2^26 bytes (GSV_E_TOO_LARGE). */
 int gsv_collation_poc_batch(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off, size_t n,
                             const uint8_t *salt, size_t salt_len, uint8_t *poc32_out);
+int gsv_collation_poc_prepare(gsv_ctx *ctx, const uint64_t *h_off, size_t n, const uint8_t *salt, size_t salt_len);
 int gsv_collation_poc_batch_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off, size_t n,
                                 const uint8_t *salt, size_t salt_len, uint8_t *d_poc32_out, void *stream);
 
@@ -242,7 +279,9 @@ int gsv_collation_header_verify_batch(gsv_ctx *ctx, const uint8_t *shard_id32, c
                                       const uint8_t *nil_flags, size_t n, uint8_t *hash32_out,
                                       uint8_t *signer20_out, uint8_t *status);
 /* Device-resident form: every array in HBM (d_nil_flags / d_hash32_out / d_signer20_out may be NULL);
- * enqueues on `stream` (NULL = the context stream) and returns. */
+ * enqueues on `stream` (NULL = the context stream) and returns.  gsv_collation_header_prepare sizes
+ * its workspace for batches of n headers. */
+int gsv_collation_header_prepare(gsv_ctx *ctx, size_t n);
 int gsv_collation_header_verify_batch_dev(gsv_ctx *ctx, const uint8_t *d_shard_id32, const uint8_t *d_chunk_root32,
                                           const uint8_t *d_period32, const uint8_t *d_proposer20,
                                           const uint8_t *d_sig65, const uint8_t *d_nil_flags, size_t n,

@@ -571,6 +571,23 @@ static int tx_decode(txdata_t *tx, const uint8_t *rlp, size_t len) {
     return 1;
 }
 
+/* Crypto provider of the Sender path.  Default: this restatement.  The CPU baseline swaps in the
+ * reference's own Keccak (ethash sha3.c) and libsecp256k1 recovery from oracle/_ref, so the timed
+ * configs[0] path is the reference's crypto (>99% of Sender's time) behind this file's RLP. */
+static or_keccak_fn g_keccak;
+static or_recover_fn g_recover;
+void oracle_set_crypto(or_keccak_fn k, or_recover_fn r) {
+    g_keccak = k;
+    g_recover = r;
+}
+static void sender_keccak(const uint8_t *in, size_t len, uint8_t out[32]) {
+    if (g_keccak) g_keccak(out, in, len);
+    else oracle_keccak256(in, len, out);
+}
+static int sender_recover(uint8_t pub[65], const uint8_t sig[65], const uint8_t h[32]) {
+    return g_recover ? g_recover(pub, sig, h) : oracle_ecrecover(pub, sig, h);
+}
+
 /* signer_kind: 0 = EIP155Signer(chain_id), 1 = HomesteadSigner, 2 = FrontierSigner
  * EIP155Signer.Hash core/types/transaction_signing.go:155-165; FrontierSigner.Hash :207-216 */
 static void tx_sighash(uint8_t out[32], const txdata_t *tx, const uint8_t *cid, size_t cidlen,
@@ -590,7 +607,7 @@ static void tx_sighash(uint8_t out[32], const txdata_t *tx, const uint8_t *cid, 
     }
     rlp_header(&all, body.n, 0xc0);
     buf_put(&all, body.p, body.n);
-    oracle_keccak256(all.p, all.n, out);
+    sender_keccak(all.p, all.n, out);
     free(body.p);
     free(all.p);
 }
@@ -629,8 +646,8 @@ int oracle_recover_plain(uint8_t addr20[20], const uint8_t sighash[32], const ui
     memcpy(sig, rb, 32);
     memcpy(sig + 32, sb, 32);
     sig[64] = V;
-    if (oracle_ecrecover(pub, sig, sighash) != 1) return OR_RECOVER_FAILED;
-    oracle_keccak256(pub + 1, 64, h);
+    if (sender_recover(pub, sig, sighash) != 1) return OR_RECOVER_FAILED;
+    sender_keccak(pub + 1, 64, h);
     memcpy(addr20, h + 12, 20);
     return OR_OK;
 }
@@ -712,6 +729,37 @@ int oracle_tx_sender(uint8_t addr20[20], const uint8_t *rlp, size_t len, const u
     txdata_t tx;
     if (!tx_decode(&tx, rlp, len)) return OR_BAD_RLP;
     return tx_sender_decoded(addr20, NULL, &tx, cid, cidlen, signer_kind);
+}
+
+/* types.Sender over n RLP txs on `threads` host threads (the configs[0] CPU baseline loop) */
+typedef struct {
+    const uint8_t *rlp;
+    const uint64_t *off;
+    long lo, hi;
+    const uint8_t *cid;
+    size_t cidlen;
+    int signer;
+    uint8_t *addr, *status;
+} sender_job;
+static void *sender_worker(void *a) {
+    sender_job *j = (sender_job *)a;
+    for (long i = j->lo; i < j->hi; i++)
+        j->status[i] = (uint8_t)oracle_tx_sender(j->addr + 20 * i, j->rlp + j->off[i], j->off[i + 1] - j->off[i],
+                                                 j->cid, j->cidlen, j->signer);
+    return NULL;
+}
+void oracle_tx_sender_many(const uint8_t *rlp, const uint64_t *off, long n, const uint8_t *cid, size_t cidlen,
+                           int signer_kind, uint8_t *addr20, uint8_t *status, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    sender_job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (sender_job){rlp, off, n * t / threads, n * (t + 1) / threads, cid, cidlen, signer_kind, addr20,
+                               status};
+        pthread_create(&th[t], NULL, sender_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
 }
 
 int oracle_tx_sighash(uint8_t out32[32], const uint8_t *rlp, size_t len, const uint8_t *cid,

@@ -40,6 +40,13 @@ int oracle_recover_plain(uint8_t addr20[20], const uint8_t sighash[32], const ui
                          const uint8_t *s, size_t slen, const uint8_t *v, size_t vlen, int homestead);
 int oracle_tx_sender(uint8_t addr20[20], const uint8_t *rlp, size_t len, const uint8_t *chain_id,
                      size_t chain_id_len, int signer_kind);
+/* Sender's Keccak / recovery provider: NULL = this restatement; the CPU baseline passes the
+ * reference's own (oracle/_ref gsvref_keccak256 / gsvref_ecrecover) */
+typedef int (*or_keccak_fn)(uint8_t *out32, const uint8_t *in, size_t len);
+typedef int (*or_recover_fn)(uint8_t *pub65, const uint8_t *sig65, const uint8_t *msg32);
+void oracle_set_crypto(or_keccak_fn k, or_recover_fn r);
+void oracle_tx_sender_many(const uint8_t *rlp, const uint64_t *off, long n, const uint8_t *cid, size_t cidlen,
+                           int signer_kind, uint8_t *addr20, uint8_t *status, int threads);
 int oracle_tx_sighash(uint8_t out32[32], const uint8_t *rlp, size_t len, const uint8_t *chain_id,
                       size_t chain_id_len, int signer_kind);
 

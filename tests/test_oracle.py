@@ -195,7 +195,7 @@ def test_bn256_algorithmic_work_figure(oracle):
     # bench.py FP_MULS_PER_CHECK: F_p products of the reference algorithm for one 4-pair check
     import bench
     g = next(x for x in golden("bn256.json")["generated"] if x["note"] == "4-pair bilinear identity (true)")
-    assert oracle.bn256_fp_muls(bytes.fromhex(g["input"])) == bench.FP_MULS_PER_CHECK
+    assert oracle.bn256_fp_muls(bytes.fromhex(g["input"])) == bench.FP_MULS_PER_CHECK_REF
 
 
 # ---------------------------------------------------------------- §8f rows 2-3: DeriveSha, POC, headers

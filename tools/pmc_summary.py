@@ -1,9 +1,10 @@
 """Summarise a tools/profile_round.sh run (rocprofv3 SQLite outputs) into one JSON per kernel.
 
-    python tools/pmc_summary.py gpurun_out/prof/<tag> > profiles/<tag>/pmc_summary.json
+    python tools/pmc_summary.py gpurun_out/prof/<tag>/<group> > profiles/<tag>/pmc_<group>.json
 
 Per kernel: dispatches, average duration (kernel-trace pass), VGPR/scratch, HBM bytes per
-dispatch from FETCH_SIZE and WRITE_SIZE (each from its own pass), and SQ VALU counters.
+dispatch from FETCH_SIZE and WRITE_SIZE (each from its own pass), SQ VALU counters and the
+integer VALU instruction counts (SQ_INSTS_VALU_INT32 / _INT64).
 gfx950 correction (MI355X_MICROARCH.md § HBM): FETCH_SIZE counts 64 B per 128-B request for
 wide coalesced reads, so `fetch_bytes_x2` doubles it; which of the two applies depends on the
 kernel's access width — both are reported, with the raw value.
@@ -55,6 +56,8 @@ def main(root):
     sq = counters(os.path.join(root, "sq", "run_results.db"),
                   {"SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
                    "GRBM_GUI_ACTIVE"})
+    ipath = os.path.join(root, "int", "run_results.db")
+    ints = counters(ipath, {"SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64"}) if os.path.exists(ipath) else {}
     for k in sorted(set(dur) | set(fetch)):
         if k.startswith("void at::") or k.startswith("__amd"):
             continue
@@ -81,6 +84,10 @@ def main(root):
                 # GRBM_GUI_ACTIVE sums the 8 XCDs' clocks; each of the 1024 SIMDs issues at most one
                 # wave-instruction per cycle: VALU wave-instructions per SIMD per cycle
                 r["valu_issue_per_simd_cycle"] = round(r["sq_insts_valu"] / (1024 * gui / 8), 4)
+        i = ints.get(k, {})
+        if i.get("SQ_INSTS_VALU_INT32"):
+            r["sq_insts_valu_int32"] = per_dispatch(i["SQ_INSTS_VALU_INT32"])
+            r["sq_insts_valu_int64"] = per_dispatch(i.get("SQ_INSTS_VALU_INT64", []))
         res[k] = r
     json.dump(res, sys.stdout, indent=1, sort_keys=True)
     print()
