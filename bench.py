@@ -52,14 +52,16 @@ MACS_PER_RECOVERY_REF = 1358 * 64 + 1729 * 36 + 301 * 64
 FP_MULS_PER_CHECK_REF = 106852            # tests/test_oracle.py pins the figure
 MACS_PER_FP_MUL = 128                      # Montgomery product: 64 + 64 partial products
 PERMS_PER_MIB = 83016                      # Keccak-f permutations per 1 MiB chunk root (data-independent)
-# Peaks (profiles/r02/microbench.txt, tools/microbench_lat.hip / microbench_int.hip on MI355X):
+# Peaks (profiles/r02/microbench_{int,lat}.txt, tools/microbench_*.hip on MI355X):
 #   VALU issue: CDNA4 SIMDs are 32 wide, a wave64 instruction issues over 2 cycles -> at most 0.5
 #   wave-instructions per SIMD per cycle (MI355X_MICROARCH.md, cdna_hip_programming.md §CDNA4).
-#   v_mad_u64_u32: sustained best 2.62 cycles per wave-instruction per SIMD (8 waves/SIMD,
-#   independent chains) -> 64 / 2.62 lanes/clk/SIMD; its nominal full-rate bound is 32.
+#   v_mad_u64_u32 (and every carry / 64-bit op) issues at a quarter of the 64-lane rate: 16
+#   lanes/clk/SIMD = 4 cycles per wave-instruction; 4.43 cycles measured with two waves per SIMD,
+#   and more waves do not raise it (k_ecrecover at 2, 3 and 4 waves/SIMD: 15.46 / 15.32 / 15.71 ms,
+#   profiles/r02/ab_ecrecover_occupancy.txt).
 VALU_ISSUE_PEAK = 0.5
 PEAK_LANE_OPS = SIMDS * 64 * VALU_ISSUE_PEAK * CLOCK          # 7.86e13 full-rate 32-bit lane-ops/s
-PEAK_MAC = SIMDS * (64 / 2.62) * CLOCK                        # 6.0e13 v_mad_u64_u32/s (measured best)
+PEAK_MAC = SIMDS * 16 * CLOCK                                 # 3.93e13 v_mad_u64_u32 lane-ops/s
 HBM_PEAK_GBPS = 8000.0
 PROFILES = os.path.join(ROOT, "profiles", "r02")
 LEGS = ["ecrecover", "chunk_root", "notary", "keccak", "tx_root", "poc", "headers", "pairing"]

@@ -140,6 +140,7 @@ GSV_DI void fp_neg(fp& r, const fp& a) {  // p - a, 0 -> 0
     }
 }
 GSV_DI void fp_mul(fp& r, const fp& a, const fp& b) {
+    GSV_OPC(gsv::OPC_BN_MUL);
     uint32_t t[8];
     uint32_t hi = mont_mul_8_asm(t, a.v, b.v, BN_P, BN_N0);
     fp_reduce_once(r, t, hi);

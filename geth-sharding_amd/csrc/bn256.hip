@@ -11,6 +11,7 @@
 //   k_bn_final    finalExponentiation (optate.go:212-261), IsOne          -> verdict per check
 // HBM layout is structure-of-arrays, word-major ([word][pair]), so each lane's word loads and
 // stores coalesce across the wave.
+#include "opcount.cuh"
 #include "bn254_dev.cuh"
 #include "gsv_internal.h"
 #include "keccak_dev.cuh"
@@ -1203,3 +1204,5 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
 }
 
 }  // namespace gsv
+
+GSV_OPCOUNT_READER(bn256)

@@ -15,6 +15,7 @@
 // k_header_compare (signer vs ProposerAddress).
 #include <hip/hip_runtime.h>
 
+#include "opcount.cuh"
 #include "gsv_internal.h"
 #include "keccak_dev.cuh"
 
@@ -169,3 +170,5 @@ hipError_t launch_header_verify(const uint8_t* d_sid32, const uint8_t* d_root32,
 }
 
 }  // namespace gsv
+
+GSV_OPCOUNT_READER(collation)

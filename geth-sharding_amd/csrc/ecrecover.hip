@@ -20,14 +20,12 @@
 //     resident, one random 80-byte entry per window, prefetched a window ahead), 16 mixed additions
 //     and no doublings (gsv_internal.h COMB_BITS).
 //   * one general Jacobian add to combine, one field inversion to affine, fused Keccak-256 address.
+#include "opcount.cuh"
 #include "recover_dev.cuh"
 
 namespace gsv {
 
 // ---------------------------------------------------------------------------- kernels
-#ifndef GSV_ECR_WAVES
-#define GSV_ECR_WAVES 2
-#endif
 // 2 waves/SIMD: two 256-thread blocks per CU share its 160 KiB LDS (72 KiB GLV table each)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAVES, GSV_ECR_WAVES))) void k_ecrecover(const uint8_t* __restrict__ msg32,
                                                    const uint8_t* __restrict__ sig65, uint32_t n,
@@ -35,7 +33,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
                                                    uint8_t* __restrict__ pub65,
                                                    uint8_t* __restrict__ addr20,
                                                    uint8_t* __restrict__ status) {
-    __shared__ uint32_t ltab[GSV_LTAB_WORDS];
+    GSV_LTAB_DECL;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t* sg = sig65 + (size_t)i * 65;
@@ -45,7 +43,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     load32_be(s, sg + 32);
     uint32_t recid = sg[64];
     fe qx, qy;
-    uint32_t st = recover_core(qx, qy, msg, r, s, recid & 3u, gtab, ltab + threadIdx.x);
+    uint32_t st = recover_core(qx, qy, msg, r, s, recid & 3u, gtab, GSV_LTAB_LANE);
     if (recid >= 4) st = GSV_ST_INVALID_RECID;
     bool ok = st == GSV_ST_OK;
     store_pub_addr(pub65 ? pub65 + (size_t)i * 65 : nullptr, addr20 ? addr20 + (size_t)i * 20 : nullptr,
@@ -63,7 +61,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
                                                 int homestead, const uint4* __restrict__ gtab,
                                                 uint8_t* __restrict__ addr20,
                                                 uint8_t* __restrict__ status) {
-    __shared__ uint32_t ltab[GSV_LTAB_WORDS];
+    GSV_LTAB_DECL;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t msg[8], r[8], s[8];
@@ -83,7 +81,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     valid = valid && !(homestead && limbs_lt(HALF_N, s));
     valid = valid && limbs_lt(r, SN) && limbs_lt(s, SN) && (V == 0 || V == 1);
     fe qx, qy;
-    uint32_t st = recover_core(qx, qy, msg, r, s, V & 1u, gtab, ltab + threadIdx.x);
+    uint32_t st = recover_core(qx, qy, msg, r, s, V & 1u, gtab, GSV_LTAB_LANE);
     if (!valid) st = GSV_ST_INVALID_SIG;
     store_pub_addr(nullptr, addr20 + (size_t)i * 20, st == GSV_ST_OK, qx, qy);
     status[i] = (uint8_t)st;
@@ -97,7 +95,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAVES, GSV_ECR_WAVES))) void k_ecrecover_precompile(
     const uint8_t* __restrict__ in128, uint32_t n, const uint4* __restrict__ gtab, uint8_t* __restrict__ out32,
     uint8_t* __restrict__ ok) {
-    __shared__ uint32_t ltab[GSV_LTAB_WORDS];
+    GSV_LTAB_DECL;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t* p = in128 + (size_t)i * 128;
@@ -118,7 +116,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     bool valid = hi == 0 && !sc_is_zero(rs) && !sc_is_zero(ss) && limbs_lt(r, SN) && limbs_lt(s, SN) &&
                  (V == 0 || V == 1);
     fe qx, qy;
-    uint32_t st = recover_core(qx, qy, msg, r, s, V & 1u, gtab, ltab + threadIdx.x);
+    uint32_t st = recover_core(qx, qy, msg, r, s, V & 1u, gtab, GSV_LTAB_LANE);
     bool good = valid && st == GSV_ST_OK;
     uint8_t* o = out32 + (size_t)i * 32;
 #pragma unroll
@@ -244,3 +242,5 @@ hipError_t launch_synth_sign(uint64_t seed, uint32_t n, const uint4* gtab, uint8
 }
 
 }  // namespace gsv
+
+GSV_OPCOUNT_READER(ecrecover)

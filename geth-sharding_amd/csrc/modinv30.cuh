@@ -17,6 +17,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "opcount.cuh"
+
 #if defined(__HIPCC__)
 #define MI30_FN __device__ __forceinline__
 #define MI30_CONST __device__ constexpr
@@ -173,6 +175,7 @@ MI30_FN void s30_to_words(uint32_t w[8], const s30& a) {
 
 // out = x^-1 mod m (x < m; 0 -> 0), words in and out
 MI30_FN void modinv30_words(uint32_t out[8], const uint32_t x[8], const modinfo30& mi) {
+    GSV_OPC(gsv::OPC_MODINV);
     s30 d, e, f, g;
 #pragma unroll
     for (int i = 0; i < 9; i++) {

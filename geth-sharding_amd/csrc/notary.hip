@@ -15,6 +15,7 @@
 //
 // The decode rules are the ones the host path uses (csrc/tx_host.hip tx_prepare), restated for one
 // lane: the blob's bytes are read through the chunk map (byte k at chunk k/31, offset 1 + k%31).
+#include "opcount.cuh"
 #include "recover_dev.cuh"
 
 namespace gsv {
@@ -236,13 +237,13 @@ GSV_DI void keccak_stream(uint64_t a[25], const PreStream& s) {
     }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_notary_tx(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAVES, GSV_ECR_WAVES))) void k_notary_tx(
     const uint8_t* __restrict__ bodies, const uint64_t* __restrict__ body_off, const BlobRec* __restrict__ blobs,
     const uint32_t* __restrict__ ntx, uint32_t max_txs, const uint8_t* __restrict__ cid64,
     const uint8_t* __restrict__ suffix, uint32_t slen, int signer_kind, const uint4* __restrict__ gtab,
     uint8_t* __restrict__ bitmap, uint32_t bm_bytes, uint8_t* __restrict__ senders,
     uint8_t* __restrict__ status_out) {
-    __shared__ uint32_t ltab[GSV_LTAB_WORDS];
+    GSV_LTAB_DECL;
     const uint32_t shard = blockIdx.y;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = min(ntx[shard], max_txs);
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     valid = valid && !sc_is_zero(rs) && !sc_is_zero(ss) && !(homestead && limbs_lt(HALF_N, s)) &&
             limbs_lt(r, SN) && limbs_lt(s, SN) && (V == 0 || V == 1);
-    uint32_t rst = recover_core(qx, qy, msg, r, s, V & 1u, gtab, ltab + threadIdx.x);
+    uint32_t rst = recover_core(qx, qy, msg, r, s, V & 1u, gtab, GSV_LTAB_LANE);
     if (st == GSV_ST_OK && !valid) st = GSV_ST_INVALID_SIG;
     if (st == GSV_ST_OK) st = rst;
     bool good = active && st == GSV_ST_OK;
@@ -584,3 +585,5 @@ hipError_t launch_notary_synth(uint64_t seed, uint32_t shard0, uint32_t n_shards
 size_t blob_rec_bytes() { return sizeof(BlobRec); }
 
 }  // namespace gsv
+
+GSV_OPCOUNT_READER(notary)

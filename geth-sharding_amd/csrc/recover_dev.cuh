@@ -37,7 +37,23 @@ __device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du
 // recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS]
 constexpr int GSV_LTAB_STRIDE = 256;
 constexpr int GSV_LTAB_WORDS = 72 * GSV_LTAB_STRIDE;
-constexpr int GLV_DIGITS = 44;  // w = 3 odd digits cover k < 2^131 (bound is 2^128)
+constexpr int GLV_DIGITS = 44;
+// where the per-lane GLV table lives: 0 = LDS ([word][256 lanes] per block), 1 = a private array
+// (scratch: memory only for resident lanes, served by L1/L2)
+#ifndef GSV_GLV_TAB
+#define GSV_GLV_TAB 0
+#endif
+// waves per SIMD the recovery kernels are compiled for (register budget 512 / waves)
+#ifndef GSV_ECR_WAVES
+#define GSV_ECR_WAVES 2
+#endif
+#if GSV_GLV_TAB == 0
+#define GSV_LTAB_DECL __shared__ uint32_t ltab[GSV_LTAB_WORDS]
+#define GSV_LTAB_LANE (ltab + threadIdx.x)
+#else
+#define GSV_LTAB_DECL
+#define GSV_LTAB_LANE nullptr
+#endif  // w = 3 odd digits cover k < 2^131 (bound is 2^128)
 
 // ---------------------------------------------------------------------------- scalar helpers
 GSV_DI void sc_from_const(sc& r, const uint32_t c[8]) {
@@ -47,6 +63,7 @@ GSV_DI void sc_from_const(sc& r, const uint32_t c[8]) {
 
 // (k * g) >> 272, rounded (libsecp256k1 scalar_8x32_impl.h mul_shift_var semantics)
 GSV_DI void sc_mul_shift272(sc& r, const sc& k, const uint32_t g[8]) {
+    GSV_OPC(OPC_SC_MUL);
     uint32_t t[16];
     mul_8x8_fx(t, k.v, g);
 #pragma unroll
@@ -323,12 +340,18 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     // conflict-free for any per-lane entry index), not in VGPRs: 72 words {x[4], y[4]} would
     // otherwise cost the kernel occupancy.  Each add loads its entry by index (no selects);
     // lambda(P) = (beta x, y) costs one product per lambda add.
+#if GSV_GLV_TAB == 1
+    uint32_t ptab[72];
+#define GLV_TAB(i) ptab[i]
+#else
+#define GLV_TAB(i) ltab[(i) * GSV_LTAB_STRIDE]
+#endif
 #pragma unroll
     for (int e = 0; e < 4; e++) {
 #pragma unroll
         for (int k = 0; k < 9; k++) {
-            ltab[(e * 9 + k) * GSV_LTAB_STRIDE] = T[e].x.v[k];
-            ltab[(36 + e * 9 + k) * GSV_LTAB_STRIDE] = T[e].y.v[k];
+            GLV_TAB(e * 9 + k) = T[e].x.v[k];
+            GLV_TAB(36 + e * 9 + k) = T[e].y.v[k];
         }
     }
 
@@ -354,8 +377,8 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             ge9 P;
 #pragma unroll
             for (int k = 0; k < 9; k++) {
-                P.x.v[k] = ltab[(xo + k) * GSV_LTAB_STRIDE];
-                P.y.v[k] = ltab[(36u + xo + k) * GSV_LTAB_STRIDE];
+                P.x.v[k] = GLV_TAB(xo + k);
+                P.y.v[k] = GLV_TAB(36u + xo + k);
             }
             if (j != 0) {  // wave-uniform
                 fe9 beta;

@@ -18,6 +18,7 @@
 #define GSV_DI __device__ __forceinline__
 
 #include "mul_asm.cuh"
+#include "opcount.cuh"
 
 namespace gsv {
 
@@ -108,6 +109,7 @@ GSV_DI void fe_reduce(fe& r, const uint32_t t[16]) {
 #define GSV_FE_FX 1
 #endif
 GSV_DI void fe_mul(fe& r, const fe& a, const fe& b) {
+    GSV_OPC(OPC_FE_MUL);
     uint32_t t[16];
 #if GSV_FE_FX
     mul_8x8_fx(t, a.v, b.v);
@@ -117,6 +119,7 @@ GSV_DI void fe_mul(fe& r, const fe& a, const fe& b) {
     fe_reduce(r, t);
 }
 GSV_DI void fe_sqr(fe& r, const fe& a) {
+    GSV_OPC(OPC_FE_SQR);
     uint32_t t[16];
 #if GSV_FE_FX
     sqr_8_fx(t, a.v);
@@ -329,11 +332,13 @@ GSV_DI void sc_reduce(sc& r, const uint32_t t[16]) {
 }
 
 GSV_DI void sc_mul(sc& r, const sc& a, const sc& b) {
+    GSV_OPC(OPC_SC_MUL);
     uint32_t t[16];
     mul_8x8_fx(t, a.v, b.v);
     sc_reduce(r, t);
 }
 GSV_DI void sc_sqr(sc& r, const sc& a) {
+    GSV_OPC(OPC_SC_SQR);
     uint32_t t[16];
     sqr_8_fx(t, a.v);
     sc_reduce(r, t);
