@@ -449,6 +449,51 @@ int oracle_secp_sign(uint8_t sig65[65], const uint8_t msg32[32], const uint8_t s
     return 1;
 }
 
+/* The GPU's synthetic signer (gsv_synth_sign, recover_dev.cuh derive32 / ecdsa_sign) restated for
+ * the configs[1] fixture: msg, key, nonce = Keccak256(le64(seed) || le64(i) || "msg"/"key"/"nce") as
+ * big-endian numbers, key and nonce reduced mod n (0 -> 1), low-s signature with its recid. */
+static void synth_derive(uint8_t out[32], uint64_t seed, uint64_t i, const char *tag) {
+    uint8_t in[19];
+    for (int b = 0; b < 8; b++) {
+        in[b] = (uint8_t)(seed >> (8 * b));
+        in[8 + b] = (uint8_t)(i >> (8 * b));
+    }
+    memcpy(in + 16, tag, 3);
+    oracle_keccak256(in, 19, out);
+}
+static void synth_mod_n(uint8_t v[32]) {
+    u256 x;
+    u256_from_be(&x, v);
+    if (u256_cmp(&x, &SECP_N) >= 0) u256_sub(&x, &x, &SECP_N);
+    if (u256_is_zero(&x)) x.v[0] = 1;
+    u256_to_be(v, &x);
+}
+typedef struct { uint64_t seed; long lo, hi; uint8_t *msg, *sig; } synth_job;
+static void *synth_worker(void *a) {
+    synth_job *j = (synth_job *)a;
+    for (long i = j->lo; i < j->hi; i++) {
+        uint8_t d[32], k[32];
+        synth_derive(j->msg + 32 * i, j->seed, (uint64_t)i, "msg");
+        synth_derive(d, j->seed, (uint64_t)i, "key");
+        synth_derive(k, j->seed, (uint64_t)i, "nce");
+        synth_mod_n(d);
+        synth_mod_n(k);
+        oracle_secp_sign(j->sig + 65 * i, j->msg + 32 * i, d, k);
+    }
+    return NULL;
+}
+void oracle_synth_sign_many(uint64_t seed, long n, uint8_t *msg32, uint8_t *sig65, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    synth_job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (synth_job){seed, n * t / threads, n * (t + 1) / threads, msg32, sig65};
+        pthread_create(&th[t], NULL, synth_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
+
 /* ===================================================================================
  * RLP (rlp/encode.go:390 writeUint, :429 writeBigInt, string/list headers) and a
  * strict decoder for txdata (core/types/transaction.go:55-70; rlp/decode.go canonical

@@ -59,6 +59,7 @@ long oracle_blob_deserialize(const uint8_t *data, size_t len, uint8_t *out, uint
                              uint8_t *skip_evm, long max_blobs);
 
 int oracle_secp_pubkey(uint8_t pub65[65], const uint8_t seckey[32]);
+void oracle_synth_sign_many(uint64_t seed, long n, uint8_t *msg32, uint8_t *sig65, int threads);
 int oracle_secp_sign(uint8_t sig65[65], const uint8_t msg32[32], const uint8_t seckey[32],
                      const uint8_t nonce32[32]);
 

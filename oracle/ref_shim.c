@@ -92,3 +92,62 @@ __attribute__((visibility("default"))) int gsvref_pubkey(unsigned char *pub65,
     if (!secp256k1_ec_pubkey_create(g_ctx, &pk, seckey32)) return 0;
     return secp256k1_ec_pubkey_serialize(g_ctx, pub65, &len, &pk, SECP256K1_EC_UNCOMPRESSED);
 }
+
+/* Signature with a caller-chosen nonce (libsecp256k1's nonce-function hook): reproduces the GPU's
+ * synthetic signer (gsv_synth_sign) with the reference's own signing code, for the configs[1]
+ * fixture.  Low-s normalised with the recid flipped, as secp256k1_ecdsa_sig_sign does. */
+static int fixed_nonce(unsigned char *nonce32, const unsigned char *msg32, const unsigned char *key32,
+                       const unsigned char *algo16, void *data, unsigned int attempt) {
+    (void)msg32;
+    (void)key32;
+    (void)algo16;
+    if (attempt) return 0;
+    memcpy(nonce32, data, 32);
+    return 1;
+}
+
+__attribute__((visibility("default"))) int gsvref_sign_nonce(unsigned char *sig65, const unsigned char *msg32,
+                                                             const unsigned char *seckey32,
+                                                             const unsigned char *nonce32) {
+    secp256k1_ecdsa_recoverable_signature s;
+    int recid = 0;
+    gsvref_init();
+    if (!secp256k1_ecdsa_sign_recoverable(g_ctx, &s, msg32, seckey32, fixed_nonce, (void *)nonce32)) return 0;
+    secp256k1_ecdsa_recoverable_signature_serialize_compact(g_ctx, sig65, &recid, &s);
+    sig65[64] = (unsigned char)recid;
+    return 1;
+}
+
+int sha3_256(uint8_t *out, size_t outlen, uint8_t const *in, size_t inlen);
+
+/* n signatures i = i0 .. i0+n-1 of the GPU's synthetic signer (gsv_synth_sign) made by the
+ * reference's code: msg / key / nonce = ethash Keccak-256(le64(seed) || le64(i) || tag), key and
+ * nonce reduced mod n by secp256k1_scalar_set_b32 (0 -> 1). */
+__attribute__((visibility("default"))) long gsvref_synth_sign_many(uint64_t seed, long i0, long n,
+                                                                   unsigned char *msg32, unsigned char *sig65) {
+    long ok = 0;
+    gsvref_init();
+    for (long j = 0; j < n; j++) {
+        uint64_t i = (uint64_t)(i0 + j);
+        unsigned char in[19], key[32], nce[32];
+        for (int b = 0; b < 8; b++) {
+            in[b] = (unsigned char)(seed >> (8 * b));
+            in[8 + b] = (unsigned char)(i >> (8 * b));
+        }
+        memcpy(in + 16, "msg", 3);
+        sha3_256(msg32 + 32 * j, 32, in, 19);
+        unsigned char *kk[2] = {key, nce};
+        const char *tags[2] = {"key", "nce"};
+        for (int t = 0; t < 2; t++) {
+            secp256k1_scalar sc;
+            int overflow = 0;
+            memcpy(in + 16, tags[t], 3);
+            sha3_256(kk[t], 32, in, 19);
+            secp256k1_scalar_set_b32(&sc, kk[t], &overflow);
+            if (secp256k1_scalar_is_zero(&sc)) secp256k1_scalar_set_int(&sc, 1);
+            secp256k1_scalar_get_b32(kk[t], &sc);
+        }
+        ok += gsvref_sign_nonce(sig65 + 65 * j, msg32 + 32 * j, key, nce);
+    }
+    return ok;
+}

@@ -220,6 +220,142 @@ def xoshiro_bytes(seed: int, n: int) -> bytes:
     return bytes(out[:n])
 
 
+def xoshiro_many(seeds, n: int):
+    """xoshiro_bytes for many seeds at once (numpy, vectorised across the streams):
+    -> uint8 array (len(seeds), n), row s == xoshiro_bytes(seeds[s], n)."""
+    import numpy as np
+    M = (1 << 64) - 1
+    st = []
+    for seed in seeds:
+        x, row = seed, []
+        for _ in range(4):
+            x = (x + 0x9E3779B97F4A7C15) & M
+            z = x
+            z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+            z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+            row.append(z ^ (z >> 31))
+        st.append(row)
+    s0, s1, s2, s3 = (np.array([r[k] for r in st], np.uint64) for k in range(4))
+    words = (n + 7) // 8
+    out = np.empty((words, len(st)), np.uint64)
+    u = np.uint64
+    with np.errstate(over="ignore"):
+        for t in range(words):
+            v = s1 * u(5)
+            out[t] = ((v << u(7)) | (v >> u(57))) * u(9)
+            tt = s1 << u(17)
+            s2 ^= s0
+            s3 ^= s1
+            s1 ^= s2
+            s0 ^= s3
+            s2 ^= tt
+            s3 = (s3 << u(45)) | (s3 >> u(19))
+    return np.ascontiguousarray(out.T).view(np.uint8)[:, :n]
+
+
+def config_fixtures():
+    """Full-size fixtures of the BASELINE.json configs (one GPU's batch each):
+      configs[0]  10,000 EIP-155 txs (oracle/cfg0.py): SHA-256 of the tx RLPs and of the senders;
+      configs[1]  the bench's 2^20 signatures (synthetic signer, seed 1000), signed by the reference's
+                  libsecp256k1 with the generator's nonces and recovered by it (oracle/_ref):
+                  SHA-256 of the 2^20 addresses (+ of the inputs), first rows;
+      configs[2]  100 xoshiro256** bodies of 1 MiB (seeds 0..99): their 100 chunk roots (restated
+                  DeriveSha, pinned by tests/test_oracle.py);
+      configs[4]  the bench's 4-pair checks (seed 5000), first 1,024: inputs rebuilt from the oracle's
+                  G1/G2 scalar multiples, verdicts from the oracle's cloudflare restatement."""
+    import ctypes
+    import hashlib
+    import threading
+
+    import numpy as np
+    from oracle import cfg0
+    R = O.ref()
+    u8 = ctypes.POINTER(ctypes.c_uint8)
+    out = {}
+
+    def par(fn, items, threads=8):
+        it = iter(items)
+        lk = threading.Lock()
+
+        def w():
+            while True:
+                with lk:
+                    x = next(it, None)
+                if x is None:
+                    return
+                fn(x)
+        ths = [threading.Thread(target=w) for _ in range(threads)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+
+    # configs[0]
+    txs, addrs = cfg0.eip155_txs(10000)
+    out["configs0_sender"] = {"n": 10000, "chain_id": 1,
+                              "txs_sha256": hashlib.sha256(b"".join(txs)).hexdigest(),
+                              "senders_sha256": hashlib.sha256(addrs.tobytes()).hexdigest(),
+                              "first": [{"rlp": h(txs[i]), "sender": h(addrs[i])} for i in range(4)]}
+    # configs[1]
+    n, seed = 1 << 20, 1000
+    R.gsvref_synth_sign_many.argtypes = [ctypes.c_uint64, ctypes.c_long, ctypes.c_long, u8, u8]
+    R.gsvref_synth_sign_many.restype = ctypes.c_long
+    msg = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 65), np.uint8)
+    pub = np.zeros((n, 65), np.uint8)
+    addr = np.zeros((n, 32), np.uint8)
+    chunks = [(c, min(n, c + 8192)) for c in range(0, n, 8192)]
+
+    def work(c):
+        lo, hi = c
+        k = hi - lo
+        assert R.gsvref_synth_sign_many(seed, lo, k, msg[lo:].ctypes.data_as(u8), sig[lo:].ctypes.data_as(u8)) == k
+        assert R.gsvref_ecrecover_many(pub[lo:].ctypes.data_as(u8), sig[lo:].ctypes.data_as(u8),
+                                       msg[lo:].ctypes.data_as(u8), k) == k
+        xy = np.ascontiguousarray(pub[lo:hi, 1:])  # Keccak256(pub[1:65]) (crypto/crypto.go:194-197)
+        off = np.arange(k + 1, dtype=np.uint64) * 64
+        R.gsvref_keccak256_many(addr[lo:].ctypes.data_as(u8), xy.ctypes.data_as(u8),
+                                off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), k)
+    par(work, chunks)
+    a20 = np.ascontiguousarray(addr[:, 12:])
+    out["configs1_ecrecover"] = {"seed": seed, "n": n, "addr_sha256": hashlib.sha256(a20.tobytes()).hexdigest(),
+                                 "msg_sha256": hashlib.sha256(msg.tobytes()).hexdigest(),
+                                 "sig_sha256": hashlib.sha256(sig.tobytes()).hexdigest(),
+                                 "first": [{"msg": h(msg[i]), "sig": h(sig[i]), "pub": h(pub[i]), "addr": h(a20[i])}
+                                           for i in range(4)]}
+    del msg, sig, pub, addr
+    # configs[2]
+    bodies = xoshiro_many(list(range(100)), 1 << 20)
+    roots = [None] * 100
+    par(lambda i: roots.__setitem__(i, O.derive_sha_bytes(bodies[i])), list(range(100)))
+    out["configs2_chunk_roots"] = {"seeds": list(range(100)), "n": 1 << 20, "roots": [h(r) for r in roots]}
+    # configs[4]
+    RR = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+    PP = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+    seed4, m = 5000, 1024
+
+    def scal(i, tag):
+        hh = O.keccak256(seed4.to_bytes(8, "little") + i.to_bytes(8, "little") + bytes([tag, 0, 0]))
+        return int.from_bytes(hh, "little") & ((1 << 253) - 1) or 1
+    checks = [None] * m
+    verdicts = [None] * m
+
+    def build(c):
+        a, b, cc, d = (scal(c, t) for t in (0x61, 0x62, 0x63, 0x64))
+        d1 = d + 1 if c % 8 == 7 else d
+        inp = (O.bn256_g1_mul(a) + O.bn256_g2_mul(b) + O.bn256_g1_mul(-b % RR) + O.bn256_g2_mul(a) +
+               O.bn256_g1_mul(cc) + O.bn256_g2_mul(d) + O.bn256_g1_mul(-d1 % RR) + O.bn256_g2_mul(cc))
+        if c % 1024 == 1023:
+            inp = inp[:384] + PP.to_bytes(32, "big") + inp[416:]
+        checks[c] = inp
+        v = O.pairing_check(inp)
+        verdicts[c] = 2 if v < 0 else v
+    par(build, list(range(m)))
+    out["configs4_pairing"] = {"seed": seed4, "n": m, "inputs_sha256": hashlib.sha256(b"".join(checks)).hexdigest(),
+                               "verdicts": "".join(str(v) for v in verdicts)}
+    dump("configs.json", out)
+
+
 def chunk_root_fixtures():
     sizes = [1, 2, 15, 16, 17, 31, 32, 127, 128, 129, 255, 256, 257, 4095, 4096, 4097, 65535, 65536, 65537]
     fills = {"random": None, "zero": 0x00, "7f": 0x7F, "80": 0x80, "ff": 0xFF}
@@ -388,7 +524,7 @@ def collation_fixtures():
 
 FIXTURES = {"keccak": keccak_fixtures, "ecrecover": ecrecover_fixtures, "tx": tx_fixtures,
             "trie": trie_fixtures, "chunk_root": chunk_root_fixtures, "bn256": bn256_fixtures,
-            "collation": collation_fixtures}
+            "collation": collation_fixtures, "configs": config_fixtures}
 
 if __name__ == "__main__":
     if not O.ref_available():

@@ -1,0 +1,88 @@
+"""GPU parity at the BASELINE.json configs' full sizes against the committed fixtures
+(tests/golden/configs.json, made by tests/golden/make_golden.py configs from the reference's own C
+code in oracle/_ref and the pinned restatement):
+
+    configs[0]  types.Sender over the 10,000 EIP-155 txs       -> SHA-256 of the senders
+    configs[1]  the bench's 2^20 signatures (seed 1000)         -> SHA-256 of the recovered addresses
+    configs[2]  100 x 1 MiB xoshiro256** bodies                 -> all 100 chunk roots
+    configs[4]  the bench's first 1,024 4-pair checks (seed 5000) -> their verdicts
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_configs1_full_batch_addresses(ctx):
+    import torch
+    g = golden("configs.json")["configs1_ecrecover"]
+    n = g["n"]
+    dev = torch.device("cuda", ctx.device)
+    msg = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sig = torch.empty((n, 65), dtype=torch.uint8, device=dev)
+    ctx.synth_sign_dev(g["seed"], msg, sig)
+    pub = torch.empty((n, 65), dtype=torch.uint8, device=dev)
+    addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    st = torch.empty((n,), dtype=torch.uint8, device=dev)
+    ctx.ecrecover_batch_dev(msg, sig, pub, addr, st)
+    torch.cuda.synchronize()
+    # the inputs are the reference signer's, byte for byte
+    assert hashlib.sha256(msg.cpu().numpy().tobytes()).hexdigest() == g["msg_sha256"]
+    assert hashlib.sha256(sig.cpu().numpy().tobytes()).hexdigest() == g["sig_sha256"]
+    assert int(st.max()) == 0
+    assert hashlib.sha256(addr.cpu().numpy().tobytes()).hexdigest() == g["addr_sha256"]
+    for i, row in enumerate(g["first"]):
+        assert bytes(pub[i].cpu().numpy()).hex() == row["pub"]
+
+
+def test_configs2_hundred_full_bodies(ctx):
+    import torch
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_golden import xoshiro_many
+    g = golden("configs.json")["configs2_chunk_roots"]
+    bodies = xoshiro_many(g["seeds"], g["n"])
+    n = len(g["seeds"])
+    dev = torch.device("cuda", ctx.device)
+    d_b = torch.from_numpy(bodies.reshape(-1)).to(dev)
+    off = np.arange(n + 1, dtype=np.uint64) * g["n"]
+    roots = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    ctx.chunk_root_batch_dev(d_b, off, roots)
+    torch.cuda.synchronize()
+    got = [bytes(r).hex() for r in roots.cpu().numpy()]
+    assert got == g["roots"]
+
+
+def test_configs4_first_1024_checks(ctx):
+    import torch
+    g = golden("configs.json")["configs4_pairing"]
+    n = g["n"]
+    dev = torch.device("cuda", ctx.device)
+    pin = torch.empty((n, 768), dtype=torch.uint8, device=dev)
+    pexp = torch.empty((n,), dtype=torch.uint8, device=dev)
+    ctx.bn256_synth_checks_dev(g["seed"], pin, pexp)
+    ver = torch.empty((n,), dtype=torch.uint8, device=dev)
+    ctx.pairing_check_batch_dev(pin, np.arange(n + 1, dtype=np.uint64) * 768, ver)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(pin.cpu().numpy().tobytes()).hexdigest() == g["inputs_sha256"]
+    want = np.array([int(c) for c in g["verdicts"]], np.uint8)
+    assert (ver.cpu().numpy() == want).all()
+    assert (pexp.cpu().numpy() == want).all()
+
+
+def test_configs0_sender(ctx, oracle):
+    if oracle.ref() is None:
+        pytest.skip("oracle/_ref not built: the configs[0] txs are signed by the reference's RFC6979 signer")
+    from oracle import cfg0
+    g = golden("configs.json")["configs0_sender"]
+    txs, want = cfg0.eip155_txs(g["n"])
+    assert hashlib.sha256(b"".join(txs)).hexdigest() == g["txs_sha256"]
+    addr, st = ctx.tx_sender_batch(txs, g["chain_id"], 0)
+    assert (st == 0).all()
+    assert hashlib.sha256(addr.tobytes()).hexdigest() == g["senders_sha256"]
