@@ -796,10 +796,10 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.o_clane = L.add((n + 1) * 4);
     s.o_cbad = L.add(n);
     s.o_pstat = L.add(np + 1);
-    s.o_pts = L.add(np * 48 * 4 + 4);
-    s.o_rs = L.add(np * 64 * 4 + 4);
+    s.o_pts = L.add(np * 54 * 4 + 4);
+    s.o_rs = L.add(np * 72 * 4 + 4);
     s.o_lstat = L.add(s.nl + 1);
-    s.o_fv = L.add(s.nl * 96 * 4 + 4);
+    s.o_fv = L.add(s.nl * 108 * 4 + 4);
     s.stage(s.o_src, pair_src.data(), np);
     s.stage(s.o_pidx, pidx.data(), np);
     s.stage(s.o_lfirst, lane_first.data(), lane_first.size());
