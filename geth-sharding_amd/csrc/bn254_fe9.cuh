@@ -362,6 +362,69 @@ FQ_FN auto fq_mul2(const fqm<La, Va>& a, const fqm<Lb, Vb>& b, const fqm<Lc, Vc>
     }
 }
 
+// REDC(sum_t a_t b_t) over N products with one reduction (N <= 6 when every operand is normalised:
+// the column bound is sum_t La_t Lb_t <= 6).  The F_p^6 product's output coordinates are such sums
+// (three F_p^2 products each), so it needs 6 reductions instead of 12 and no intermediate additions.
+template <int N>
+FQ_FN void fq_redc_n(uint32_t r[9], const uint32_t (&a)[N][9], const uint32_t (&b)[N][9]) {
+    uint32_t m[9];
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; k++) {
+#pragma unroll
+        for (int t = 0; t < N; t++) {
+#pragma unroll
+            for (int i = 0; i < 9; i++) {
+                int j = k - i;
+                if (j >= 0 && j < 9) acc += (uint64_t)a[t][i] * b[t][j];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            int j = k - i;
+            if (i < k && j >= 0 && j < 9) acc += (uint64_t)m[i] * FQ_P[j];
+        }
+        if (k < 9) {
+            m[k] = ((uint32_t)acc * FQ_N0) & FQ_M29;
+            acc += (uint64_t)m[k] * FQ_P[0];
+        } else {
+            r[k - 9] = (uint32_t)acc & FQ_M29;
+        }
+        acc >>= 29;
+    }
+    r[8] = (uint32_t)acc;
+}
+template <class T>
+struct fq_traits;
+template <int L, int V>
+struct fq_traits<fqm<L, V>> {
+    static constexpr int l = L, v = V;
+};
+// fq_dot(a0, b0, a1, b1, ...) = (a0 b0 + a1 b1 + ...) R^-1: operands' bounds checked at compile time
+template <class... T>
+FQ_FN auto fq_dot(const T&... xs) {
+    constexpr int N = (int)sizeof...(T) / 2;
+    constexpr int Ls[] = {fq_traits<T>::l...};
+    constexpr int Vs[] = {fq_traits<T>::v...};
+    constexpr int LL = [&] { int s = 0; for (int t = 0; t < N; t++) s += Ls[2 * t] * Ls[2 * t + 1]; return s; }();
+    constexpr int S = [&] { int s = 0; for (int t = 0; t < N; t++) s += Vs[2 * t] * Vs[2 * t + 1]; return s; }();
+    static_assert(2 * N == (int)sizeof...(T) && LL <= 6 && S <= FQ_PROD_MAX, "fq_dot operand bounds");
+    const uint32_t* p[] = {xs.v...};
+    uint32_t A[N][9], B[N][9];
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+        GSV_OPC(gsv::OPC_BN_MUL);
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            A[t][i] = p[2 * t][i];
+            B[t][i] = p[2 * t + 1][i];
+        }
+    }
+    fqm<1, S / 168 + 2> r;
+    fq_redc_n<N>(r.v, A, B);
+    return r;
+}
+
 // ---------------------------------------------------------------------------- conversions / tests
 FQ_FN fqm<1, 1> fq_const(const uint32_t c[9]) {
     fqm<1, 1> r;
@@ -416,12 +479,6 @@ FQ_FN fqm<L2, V2> fq_widen(const fqm<L, V>& a) {
     for (int i = 0; i < 9; i++) r.v[i] = a.v[i];
     return r;
 }
-template <class T>
-struct fq_traits;
-template <int L, int V>
-struct fq_traits<fqm<L, V>> {
-    static constexpr int l = L, v = V;
-};
 
 // ============================================================================ F_p^2 (gfp2.go): x i + y
 template <int L, int V>
@@ -532,55 +589,106 @@ FQ_FN fp2 fp2_inv(const fp2m<L, V>& a) {
 }
 
 // ============================================================================ F_p^6 (gfp6.go): x tau^2 + y tau + z
-struct fp6 {
-    fp2 x, y, z;
+// fp6t<E>: coordinates of F_p^2 type E (lazy bounds); fp6 is the stored form
+template <class E>
+struct fp6t {
+    E x, y, z;
 };
+using fp6 = fp6t<fp2>;
+template <class T>
+struct fp2_traits;
+template <int L, int V>
+struct fp2_traits<fp2m<L, V>> {
+    static constexpr int l = L, v = V;
+};
+template <int L2, int V2, int L, int V>
+FQ_FN fp2m<L2, V2> fp2_widen(const fp2m<L, V>& a) { return fp2m<L2, V2>{fq_widen<L2, V2>(a.x), fq_widen<L2, V2>(a.y)}; }
+// three coordinates -> one F_p^6 element of their common bound
+template <class X, class Y, class Z>
+FQ_FN auto fp6_of(const X& x, const Y& y, const Z& z) {
+    constexpr int l = imax(imax(fp2_traits<X>::l, fp2_traits<Y>::l), fp2_traits<Z>::l);
+    constexpr int v = imax(imax(fp2_traits<X>::v, fp2_traits<Y>::v), fp2_traits<Z>::v);
+    return fp6t<fp2m<l, v>>{fp2_widen<l, v>(x), fp2_widen<l, v>(y), fp2_widen<l, v>(z)};
+}
+template <class E>
+FQ_FN fp6 fp6_store(const fp6t<E>& a) { return fp6{fp2_store(a.x), fp2_store(a.y), fp2_store(a.z)}; }
+template <class E>
+FQ_FN auto fp6_normalize(const fp6t<E>& a) { return fp6_of(fp2_normalize(a.x), fp2_normalize(a.y), fp2_normalize(a.z)); }
 FQ_FN fp6 fp6_zero() { return fp6{fp2_zero(), fp2_zero(), fp2_zero()}; }
 FQ_FN fp6 fp6_one() { return fp6{fp2_zero(), fp2_zero(), fp2_one()}; }
-FQ_FN fp6 fp6_neg(const fp6& a) { return fp6{fp2_store(fp2_neg(a.x)), fp2_store(fp2_neg(a.y)), fp2_store(fp2_neg(a.z))}; }
-FQ_FN fp6 fp6_add(const fp6& a, const fp6& b) {
-    return fp6{fp2_store(fp2_add(a.x, b.x)), fp2_store(fp2_add(a.y, b.y)), fp2_store(fp2_add(a.z, b.z))};
+template <class A>
+FQ_FN auto fp6_neg(const fp6t<A>& a) { return fp6_of(fp2_neg(a.x), fp2_neg(a.y), fp2_neg(a.z)); }
+template <class A, class B>
+FQ_FN auto fp6_add(const fp6t<A>& a, const fp6t<B>& b) {
+    return fp6_of(fp2_add(a.x, b.x), fp2_add(a.y, b.y), fp2_add(a.z, b.z));
 }
-FQ_FN fp6 fp6_sub(const fp6& a, const fp6& b) {
-    return fp6{fp2_store(fp2_sub(a.x, b.x)), fp2_store(fp2_sub(a.y, b.y)), fp2_store(fp2_sub(a.z, b.z))};
+template <class A, class B>
+FQ_FN auto fp6_sub(const fp6t<A>& a, const fp6t<B>& b) {
+    return fp6_of(fp2_sub(a.x, b.x), fp2_sub(a.y, b.y), fp2_sub(a.z, b.z));
 }
 // gfp6.go:140-149: tau (x tau^2 + y tau + z) = y tau^2 + z tau + x xi
-FQ_FN fp6 fp6_mul_tau(const fp6& a) { return fp6{a.y, a.z, fp2_store(fp2_mul_xi(a.x))}; }
-// gfp6.go:96-123 (Karatsuba; the same field element as the reference's product)
-FQ_FN fp6 fp6_mul(const fp6& a, const fp6& b) {
-    auto v0 = fp2_mul(a.z, b.z);
-    auto v1 = fp2_mul(a.y, b.y);
-    auto v2 = fp2_mul(a.x, b.x);
-    auto tz = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.x, a.y), fp2_add(b.x, b.y)), v1), v2)), v0);
-    auto ty = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.y, a.z), fp2_add(b.y, b.z)), v0), v1), fp2_mul_xi(v2));
-    auto tx = fp2_sub(fp2_add(fp2_sub(fp2_mul(fp2_add(a.x, a.z), fp2_add(b.x, b.z)), v0), v1), v2);
-    return fp6{fp2_store(tx), fp2_store(ty), fp2_store(tz)};
+template <class A>
+FQ_FN auto fp6_mul_tau(const fp6t<A>& a) { return fp6_of(a.y, a.z, fp2_mul_xi(a.x)); }
+
+// gfp6.go:96-123.  The reference's product, with each output coordinate's three F_p^2 products
+// summed before one reduction (fq_dot over six F_p products per F_p coordinate): with u = a.i,
+// v = b.j, [u v] = (ux vy + uy vx) i + (uy vy + (-ux) vx), and xi folded into b:
+//   c.x = a.x b.z + a.y b.y + a.z b.x,  c.y = a.y b.z + a.z b.y + a.x (xi b.x),
+//   c.z = a.z b.z + a.x (xi b.y) + a.y (xi b.x).
+// Operands are brought to limb bound 1 (normalised) and, if their value bounds would overflow the
+// six-term sum, reduced.
+template <class A, class B>
+FQ_FN auto fp6_mul(const fp6t<A>& a_, const fp6t<B>& b_) {
+    constexpr int va = fp2_traits<A>::v, vb = fp2_traits<B>::v;
+    if constexpr (6 * va * (vb + 2) > FQ_PROD_MAX || 6 * va * 34 > FQ_PROD_MAX) {
+        if constexpr (va >= vb) return fp6_mul(fp6_of(fp2_of(fq_reduce(a_.x.x), fq_reduce(a_.x.y)), fp2_of(fq_reduce(a_.y.x), fq_reduce(a_.y.y)), fp2_of(fq_reduce(a_.z.x), fq_reduce(a_.z.y))), b_);
+        else return fp6_mul(a_, fp6_of(fp2_of(fq_reduce(b_.x.x), fq_reduce(b_.x.y)), fp2_of(fq_reduce(b_.y.x), fq_reduce(b_.y.y)), fp2_of(fq_reduce(b_.z.x), fq_reduce(b_.z.y))));
+    } else {
+        auto a = fp6_normalize(a_);
+        auto b = fp6_normalize(b_);
+        auto nax = fq_normalize(fq_neg(a.x.x)), nay = fq_normalize(fq_neg(a.y.x)), naz = fq_normalize(fq_neg(a.z.x));
+        auto xbx = fp2_normalize(fp2_mul_xi(b.x)), xby = fp2_normalize(fp2_mul_xi(b.y));
+        auto cxx = fq_dot(a.x.x, b.z.y, a.x.y, b.z.x, a.y.x, b.y.y, a.y.y, b.y.x, a.z.x, b.x.y, a.z.y, b.x.x);
+        auto cxy = fq_dot(a.x.y, b.z.y, nax, b.z.x, a.y.y, b.y.y, nay, b.y.x, a.z.y, b.x.y, naz, b.x.x);
+        auto cyx = fq_dot(a.y.x, b.z.y, a.y.y, b.z.x, a.z.x, b.y.y, a.z.y, b.y.x, a.x.x, xbx.y, a.x.y, xbx.x);
+        auto cyy = fq_dot(a.y.y, b.z.y, nay, b.z.x, a.z.y, b.y.y, naz, b.y.x, a.x.y, xbx.y, nax, xbx.x);
+        auto czx = fq_dot(a.z.x, b.z.y, a.z.y, b.z.x, a.x.x, xby.y, a.x.y, xby.x, a.y.x, xbx.y, a.y.y, xbx.x);
+        auto czy = fq_dot(a.z.y, b.z.y, naz, b.z.x, a.x.y, xby.y, nax, xby.x, a.y.y, xbx.y, nay, xbx.x);
+        return fp6_of(fp2_of(cxx, cxy), fp2_of(cyx, cyy), fp2_of(czx, czy));
+    }
 }
-// a * (by tau + bz): a line's sparse factor (x coefficient 0), 5 F_p^2 products instead of 6
-FQ_FN fp6 fp6_mul_sparse(const fp6& a, const fp2& by, const fp2& bz) {
-    auto v0 = fp2_mul(a.z, bz);
-    auto v1 = fp2_mul(a.y, by);
-    auto tz = fp2_add(fp2_mul_xi(fp2_mul(a.x, by)), v0);  // tau^3 = xi
-    auto ty = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.y, a.z), fp2_add(by, bz)), v0), v1);
-    auto tx = fp2_add(fp2_mul(a.x, bz), v1);
-    return fp6{fp2_store(tx), fp2_store(ty), fp2_store(tz)};
+// a * (by tau + bz): a line's sparse factor (x coefficient 0), four F_p products per coordinate:
+//   c.x = a.x bz + a.y by,  c.y = a.y bz + a.z by,  c.z = a.z bz + a.x (xi by)
+template <class A, int L1, int V1, int L2, int V2>
+FQ_FN auto fp6_mul_sparse(const fp6t<A>& a_, const fp2m<L1, V1>& by_, const fp2m<L2, V2>& bz_) {
+    constexpr int va = fp2_traits<A>::v, vb = imax(imax(V1, V2), 34);
+    if constexpr (4 * va * (vb + 2) > FQ_PROD_MAX) {
+        return fp6_mul_sparse(fp6_of(fp2_of(fq_reduce(a_.x.x), fq_reduce(a_.x.y)), fp2_of(fq_reduce(a_.y.x), fq_reduce(a_.y.y)), fp2_of(fq_reduce(a_.z.x), fq_reduce(a_.z.y))), by_, bz_);
+    } else {
+        auto a = fp6_normalize(a_);
+        auto by = fp2_normalize(by_);
+        auto bz = fp2_normalize(bz_);
+        auto nax = fq_normalize(fq_neg(a.x.x)), nay = fq_normalize(fq_neg(a.y.x)), naz = fq_normalize(fq_neg(a.z.x));
+        auto xby = fp2_normalize(fp2_mul_xi(by));
+        auto cxx = fq_dot(a.x.x, bz.y, a.x.y, bz.x, a.y.x, by.y, a.y.y, by.x);
+        auto cxy = fq_dot(a.x.y, bz.y, nax, bz.x, a.y.y, by.y, nay, by.x);
+        auto cyx = fq_dot(a.y.x, bz.y, a.y.y, bz.x, a.z.x, by.y, a.z.y, by.x);
+        auto cyy = fq_dot(a.y.y, bz.y, nay, bz.x, a.z.y, by.y, naz, by.x);
+        auto czx = fq_dot(a.z.x, bz.y, a.z.y, bz.x, a.x.x, xby.y, a.x.y, xby.x);
+        auto czy = fq_dot(a.z.y, bz.y, naz, bz.x, a.x.y, xby.y, nax, xby.x);
+        return fp6_of(fp2_of(cxx, cxy), fp2_of(cyx, cyy), fp2_of(czx, czy));
+    }
 }
-FQ_FN fp6 fp6_mul_fp2(const fp6& a, const fp2& b) {
-    return fp6{fp2_store(fp2_mul(a.x, b)), fp2_store(fp2_mul(a.y, b)), fp2_store(fp2_mul(a.z, b))};
+template <class A, int L, int V>
+FQ_FN auto fp6_mul_fp2(const fp6t<A>& a, const fp2m<L, V>& b) {
+    return fp6_of(fp2_mul(a.x, b), fp2_mul(a.y, b), fp2_mul(a.z, b));
 }
-FQ_FN fp6 fp6_mul_fp(const fp6& a, const fq& b) {
-    return fp6{fp2_store(fp2_mul_fp(a.x, b)), fp2_store(fp2_mul_fp(a.y, b)), fp2_store(fp2_mul_fp(a.z, b))};
+template <class A, int L, int V>
+FQ_FN auto fp6_mul_fp(const fp6t<A>& a, const fqm<L, V>& b) {
+    return fp6_of(fp2_mul_fp(a.x, b), fp2_mul_fp(a.y, b), fp2_mul_fp(a.z, b));
 }
-// gfp6.go:151-170
-FQ_FN fp6 fp6_sqr(const fp6& a) {
-    auto v0 = fp2_sqr(a.z);
-    auto v1 = fp2_sqr(a.y);
-    auto v2 = fp2_sqr(a.x);
-    auto c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_sqr(fp2_add(a.x, a.y)), v1), v2)), v0);
-    auto c1 = fp2_add(fp2_sub(fp2_sub(fp2_sqr(fp2_add(a.y, a.z)), v0), v1), fp2_mul_xi(v2));
-    auto c2 = fp2_sub(fp2_add(fp2_sub(fp2_sqr(fp2_add(a.x, a.z)), v0), v1), v2);
-    return fp6{fp2_store(c2), fp2_store(c1), fp2_store(c0)};
-}
+template <class A>
+FQ_FN auto fp6_sqr(const fp6t<A>& a) { return fp6_mul(a, a); }
 // gfp6.go:54-62
 FQ_FN fp6 fp6_frob(const fp6& a) {
     return fp6{fp2_store(fp2_mul(fp2_conj(a.x), fp2_const(FQ_XI_2P2_3_X, FQ_XI_2P2_3_Y))),

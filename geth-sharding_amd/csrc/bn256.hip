@@ -55,11 +55,11 @@ GSV_DI bool fp12_is_one(const fp12& e) {
             (int)fp2_is_zero(e.y.y) & (int)fq_is_zero(e.y.z.x);
     return (z & (int)fq_eq(e.y.z.y, fq_const(FQ_ONE))) != 0;
 }
-GSV_DI fp12 fp12_conj(const fp12& a) { return fp12{fp6_neg(a.x), a.y}; }
+GSV_DI fp12 fp12_conj(const fp12& a) { return fp12{fp6_store(fp6_neg(a.x)), a.y}; }
 // gfp12.go:60-66
 static BN_NI void fp12_frob_p(fp12* pe, const fp12* pa) {
     const fp12 a = *pa;
-    pe->x = fp6_mul_fp2(fp6_frob(a.x), fp2_const(FQ_XI_P1_6_X, FQ_XI_P1_6_Y));
+    pe->x = fp6_store(fp6_mul_fp2(fp6_frob(a.x), fp2_const(FQ_XI_P1_6_X, FQ_XI_P1_6_Y)));
     pe->y = fp6_frob(a.y);
 }
 GSV_DI fp12 fp12_frob(const fp12& a) {
@@ -70,7 +70,7 @@ GSV_DI fp12 fp12_frob(const fp12& a) {
 // gfp12.go:68-74
 static BN_NI void fp12_frob_p2_p(fp12* pe, const fp12* pa) {
     const fp12 a = *pa;
-    pe->x = fp6_mul_fp(fp6_frob_p2(a.x), fq_c(FQ_XI_PSQ1_6));
+    pe->x = fp6_store(fp6_mul_fp(fp6_frob_p2(a.x), fq_c(FQ_XI_PSQ1_6)));
     pe->y = fp6_frob_p2(a.y);
 }
 GSV_DI fp12 fp12_frob_p2(const fp12& a) {
@@ -81,10 +81,10 @@ GSV_DI fp12 fp12_frob_p2(const fp12& a) {
 // gfp12.go:94-106.  Karatsuba over F_p^6: x = (a.x + a.y)(b.x + b.y) - a.x b.x - a.y b.y equals the
 // reference's a.x b.y + b.x a.y (3 F_p^6 products instead of 4, the same field element).
 GSV_DI fp12 fp12_mul_i(const fp12& a, const fp12& b) {
-    fp6 v0 = fp6_mul(a.x, b.x);
-    fp6 v1 = fp6_mul(a.y, b.y);
-    fp6 tx = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.x, a.y), fp6_add(b.x, b.y)), v0), v1);
-    return fp12{tx, fp6_add(v1, fp6_mul_tau(v0))};
+    auto v0 = fp6_mul(a.x, b.x);
+    auto v1 = fp6_mul(a.y, b.y);
+    fp6 tx = fp6_store(fp6_sub(fp6_sub(fp6_mul(fp6_add(a.x, a.y), fp6_add(b.x, b.y)), v0), v1));
+    return fp12{tx, fp6_store(fp6_add(v1, fp6_mul_tau(v0)))};
 }
 static BN_NI void fp12_mul_p(fp12* pe, const fp12* pa, const fp12* pb) { *pe = fp12_mul_i(*pa, *pb); }
 GSV_DI fp12 fp12_mul(const fp12& a, const fp12& b) {
@@ -94,10 +94,10 @@ GSV_DI fp12 fp12_mul(const fp12& a, const fp12& b) {
 }
 // gfp12.go:129-143
 GSV_DI fp12 fp12_sqr_i(const fp12& a) {
-    fp6 v0 = fp6_mul(a.x, a.y);
-    fp6 t = fp6_add(fp6_mul_tau(a.x), a.y);
-    fp6 ty = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.x, a.y), t), v0), fp6_mul_tau(v0));
-    return fp12{fp6_add(v0, v0), ty};
+    fp6 v0 = fp6_store(fp6_mul(a.x, a.y));
+    auto t = fp6_add(fp6_mul_tau(a.x), a.y);
+    fp6 ty = fp6_store(fp6_sub(fp6_sub(fp6_mul(fp6_add(a.x, a.y), t), v0), fp6_mul_tau(v0)));
+    return fp12{fp6_store(fp6_add(v0, v0)), ty};
 }
 // Squaring in the cyclotomic subgroup (Granger-Scott, "Faster squaring in the cyclotomic subgroup of
 // sixth degree extensions", PKC 2010): 9 F_p^2 squarings instead of two F_p^6 products.  Valid for
@@ -143,10 +143,10 @@ GSV_DI fp12 fp12_cyclo_sqr(const fp12& a) {
 // gfp12.go:145-160
 static BN_NI void fp12_inv_p(fp12* pe, const fp12* pa) {
     const fp12 a = *pa;
-    fp6 t1 = fp6_sub(fp6_sqr(a.y), fp6_mul_tau(fp6_sqr(a.x)));
+    fp6 t1 = fp6_store(fp6_sub(fp6_sqr(a.y), fp6_mul_tau(fp6_sqr(a.x))));
     fp6 t2 = fp6_inv(t1);
-    pe->x = fp6_mul(fp6_neg(a.x), t2);
-    pe->y = fp6_mul(a.y, t2);
+    pe->x = fp6_store(fp6_mul(fp6_neg(a.x), t2));
+    pe->y = fp6_store(fp6_mul(a.y, t2));
 }
 // gfp12.go:113-127 with power = u; only called on cyclotomic-subgroup elements (the final
 // exponentiation's hard part), where a^-1 = conj(a): the NAF of u needs 23 products instead of the
@@ -159,7 +159,7 @@ static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
         bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
         if (pos || neg) {
             fp12 t = *a;
-            if (neg) t.x = fp6_neg(t.x);
+            if (neg) t.x = fp6_store(fp6_neg(t.x));
             sum = fp12_mul(sum, t);
         }
     }
@@ -214,13 +214,13 @@ static BN_NI void fp12_cyclo_sqr3(fp12* pe, const fp12* pa, int role, int base) 
 // fp12_mul_i's three F_p^6 products, one per role
 static BN_NI void fp12_mul3(fp12* pe, const fp12* pa, const fp12* pb, int role, int base) {
     const fp12 a = *pa, b = *pb;
-    fp6 sa = fp6_add(a.x, a.y), sb = fp6_add(b.x, b.y);
+    fp6 sa = fp6_store(fp6_add(a.x, a.y)), sb = fp6_store(fp6_add(b.x, b.y));
     fp6 l = role == 0 ? a.x : role == 1 ? a.y : sa;
     fp6 r = role == 0 ? b.x : role == 1 ? b.y : sb;
-    fp6 prod = fp6_mul(l, r), v[3];
+    fp6 prod = fp6_store(fp6_mul(l, r)), v[3];
     gather3(v, prod, base);
-    pe->x = fp6_sub(fp6_sub(v[2], v[0]), v[1]);
-    pe->y = fp6_add(v[1], fp6_mul_tau(v[0]));
+    pe->x = fp6_store(fp6_sub(fp6_sub(v[2], v[0]), v[1]));
+    pe->y = fp6_store(fp6_add(v[1], fp6_mul_tau(v[0])));
 }
 static BN_NI void fp12_exp_u3(fp12* c, const fp12* a, int role, int base) {
     fp12 sum = *a;
@@ -230,7 +230,7 @@ static BN_NI void fp12_exp_u3(fp12* c, const fp12* a, int role, int base) {
         bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
         if (pos || neg) {
             fp12 t = *a;
-            if (neg) t.x = fp6_neg(t.x);
+            if (neg) t.x = fp6_store(fp6_neg(t.x));
             fp12_mul3(&sum, &sum, &t, role, base);
         }
     }
@@ -399,12 +399,11 @@ GSV_DI line line_double_i(g2j& r, const g1a& q) {
 // optate.go:94-112: ret * (x = (0, a, b), y = (0, 0, c))
 GSV_DI void mul_line_i(fp12& ret, const line& l) {
     // ordered (in place) so that at most ret + one F_p^6 temporary + the line are live at a time
-    fp6 a2 = fp6_mul_sparse(ret.x, l.a, l.b);           // (0, a, b) * ret.x
-    ret.x = fp6_add(ret.x, ret.y);                      // s = ret.x + ret.y
-    ret.y = fp6_mul_fp2(ret.y, l.c);                    // t3
-    ret.x = fp6_mul_sparse(ret.x, l.a, s2(fp2_add(l.b, l.c)));  // s * (0, a, b + c)
-    ret.x = fp6_sub(fp6_sub(ret.x, a2), ret.y);
-    ret.y = fp6_add(ret.y, fp6_mul_tau(a2));
+    fp6 a2 = fp6_store(fp6_mul_sparse(ret.x, l.a, l.b));  // (0, a, b) * ret.x
+    auto s = fp6_add(ret.x, ret.y);                        // ret.x + ret.y
+    fp6 t3 = fp6_store(fp6_mul_fp2(ret.y, l.c));
+    ret.x = fp6_store(fp6_sub(fp6_sub(fp6_mul_sparse(s, l.a, fp2_add(l.b, l.c)), a2), t3));  // s * (0, a, b + c)
+    ret.y = fp6_store(fp6_add(t3, fp6_mul_tau(a2)));
 }
 static BN_NI void mul_line_p(fp12* ret, const line* l) { mul_line_i(*ret, *l); }
 

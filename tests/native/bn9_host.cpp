@@ -57,7 +57,13 @@ extern "C" void h_mul_small8(uint32_t* r, int* lv, const uint32_t* a) { st(r, lv
 static fp2 ld2(const uint32_t* a) { return fp2{ld<1, VS>(a), ld<1, VS>(a + 9)}; }
 static void st2(uint32_t* r, const fp2& x) { for (int i = 0; i < 9; i++) { r[i] = x.x.v[i]; r[9 + i] = x.y.v[i]; } }
 static fp6 ld6(const uint32_t* a) { return fp6{ld2(a), ld2(a + 18), ld2(a + 36)}; }
-static void st6(uint32_t* r, const fp6& x) { st2(r, x.x); st2(r + 18, x.y); st2(r + 36, x.z); }
+template <class E>
+static void st6(uint32_t* r, const fp6t<E>& x0) {
+    fp6 x = fp6_store(x0);
+    st2(r, x.x);
+    st2(r + 18, x.y);
+    st2(r + 36, x.z);
+}
 extern "C" int h_vs() { return VS; }
 extern "C" void h_fp2_mul(uint32_t* r, const uint32_t* a, const uint32_t* b) { st2(r, fp2_store(fp2_mul(ld2(a), ld2(b)))); }
 extern "C" void h_fp2_sqr(uint32_t* r, const uint32_t* a) { st2(r, fp2_store(fp2_sqr(ld2(a)))); }
@@ -72,3 +78,19 @@ extern "C" void h_fp6_inv(uint32_t* r, const uint32_t* a) { st6(r, fp6_inv(ld6(a
 extern "C" void h_fp6_frob(uint32_t* r, const uint32_t* a) { st6(r, fp6_frob(ld6(a))); }
 extern "C" void h_fp6_frob_p2(uint32_t* r, const uint32_t* a) { st6(r, fp6_frob_p2(ld6(a))); }
 extern "C" void h_fp6_mul_tau(uint32_t* r, const uint32_t* a) { st6(r, fp6_mul_tau(ld6(a))); }
+// lazy operands: F_p^6 products of sums (value bound 64, limb bound 2) and a six-term dot product
+// at its largest admissible bounds
+extern "C" void h_fp6_mul_sums(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* c, const uint32_t* d) {
+    st6(r, fp6_mul(fp6_add(ld6(a), ld6(b)), fp6_add(ld6(c), ld6(d))));
+}
+extern "C" void h_fp6_sparse_sum(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* by, const uint32_t* bz) {
+    st6(r, fp6_mul_sparse(fp6_add(ld6(a), ld6(b)), ld2(by), fp2_add(ld2(by), ld2(bz))));
+}
+extern "C" void h_fp6_sub_tau(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+    st6(r, fp6_sub(fp6_mul_tau(ld6(a)), fp6_neg(ld6(b))));
+}
+extern "C" void h_dot6(uint32_t* r, int* lv, const uint32_t* x) {
+    st(r, lv, fq_dot(ld<1, 64>(x), ld<1, 64>(x + 9), ld<1, 64>(x + 18), ld<1, 64>(x + 27), ld<1, 64>(x + 36),
+                     ld<1, 64>(x + 45), ld<1, 64>(x + 54), ld<1, 64>(x + 63), ld<1, 64>(x + 72), ld<1, 64>(x + 81),
+                     ld<1, 64>(x + 90), ld<1, 64>(x + 99)));
+}

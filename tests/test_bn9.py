@@ -130,6 +130,18 @@ def test_reduce_canon_normalize_neg(lib):
         assert (val(r) - 8 * val(a)) % P == 0
 
 
+def test_dot6_bounds_and_values(lib):
+    rng = random.Random(28)
+    r, lv = U9(), I2()
+    U108 = ctypes.c_uint32 * 108
+    for _ in range(400):
+        xs = [rnd(rng, 1, 64) for _ in range(12)]
+        lib.h_dot6(r, lv, U108(*sum(xs, [])))
+        check(r, lv)
+        want = sum(val(xs[2 * t]) * val(xs[2 * t + 1]) for t in range(6)) * RINV % P
+        assert val(r) % P == want
+
+
 def test_inverse(lib):
     rng = random.Random(25)
     r, lv = U9(), I2()
@@ -268,3 +280,26 @@ def test_fp6(lib):
         assert dec6(r) == ap
         lib.h_fp6_frob_p2(r, la)
         assert dec6(r) == f6pow(ap, P)
+
+
+def f6add(a, b):
+    return tuple(f2add(x, y) for x, y in zip(a, b))
+
+
+def test_fp6_lazy_operands(lib):
+    rng = random.Random(29)
+    U54, U18 = ctypes.c_uint32 * 54, ctypes.c_uint32 * 18
+    r = U54()
+    for _ in range(100):
+        a, b, c, d = rnd6(rng), rnd6(rng), rnd6(rng), rnd6(rng)
+        la, lb, lc, ld = (U54(*enc6(rng, v)) for v in (a, b, c, d))
+        lib.h_fp6_mul_sums(r, la, lb, lc, ld)
+        stored(list(r))
+        assert dec6(r) == f6mul(f6add(a, b), f6add(c, d))
+        y, z = rnd2(rng), rnd2(rng)
+        lib.h_fp6_sparse_sum(r, la, lb, U18(*enc2(rng, y)), U18(*enc2(rng, z)))
+        stored(list(r))
+        assert dec6(r) == f6mul(f6add(a, b), ((0, 0), y, f2add(y, z)))
+        lib.h_fp6_sub_tau(r, la, lb)
+        stored(list(r))
+        assert dec6(r) == f6add(f6mul(a, ((0, 0), (0, 1), (0, 0))), b)
