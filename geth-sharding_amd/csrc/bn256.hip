@@ -3,11 +3,15 @@
 //
 // One lane per pair for decode + G2 subgroup check, one lane per check for the multi-Miller loop
 // and the final exponentiation.  Three launches:
-//   k_bn_prepare  decode the 192-byte pair (bn256.go:120-164 G1.Unmarshal, :256-306 G2.Unmarshal):
+//   k_bn_prepare  two wave roles per 64 pairs, running concurrently:
+//                 (0) decode the 192-byte pair (bn256.go:120-164 G1.Unmarshal, :256-306 G2.Unmarshal):
 //                 coordinates < p, Montgomery encode, infinity detection, y^2 = x^3 + 3 on G1,
-//                 on-twist + subgroup membership on G2 (twist.go:47-63)  -> pair status + points
+//                 on-twist + subgroup membership on G2 (twist.go:47-63)  -> pair status + points;
+//                 (1) the pair's 91 Miller-loop lines (optate.go:3-92, 122-210: the twist point's
+//                 doubling / addition steps evaluated at P)                  -> line coefficients
 //   k_bn_miller   optimal-ate Miller loop (optate.go:122-210) over all of a check's pairs with one
-//                 shared accumulator (the product of the per-pair values) -> F_p^12 per check
+//                 shared accumulator (the product of the per-pair values), multiplying in the
+//                 precomputed lines                                          -> F_p^12 per check
 //   k_bn_final    finalExponentiation (optate.go:212-261), IsOne          -> verdict per check
 // The field arithmetic is bn254_fe9.cuh: 9 x 29-bit limbs, Montgomery R = 2^261, lazily reduced —
 // elements are congruent to, not equal to, the reference's gfP words, so every decision (equality,
@@ -491,21 +495,17 @@ GSV_DI void fp12_store(uint32_t* base, uint32_t n, uint32_t i, const fp12& e) {
 #pragma unroll
     for (int k = 0; k < 12; k++) soa_store(base, n, i, k, f[k]);
 }
-GSV_DI g2j g2j_load(const uint32_t* __restrict__ base, uint32_t n, uint32_t i) {
-    return g2j{soa_load2(base, n, i, 0), soa_load2(base, n, i, 2), soa_load2(base, n, i, 4), soa_load2(base, n, i, 6)};
+// lines per pair: 64 doublings, one addition per nonzero NAF digit, the two Frobenius additions
+constexpr int BN_NLINES = 64 + __builtin_popcountll(NAF_POS | NAF_NEG) + 2;
+static_assert(BN_NLINES == 91, "sixuPlus2NAF has 25 nonzero digits below the leading one");
+// line li of pair j: 6 F_p elements (a, b, c) in a [BN_NLINES * 54 words][npairs] array
+GSV_DI void line_store(uint32_t* __restrict__ lines, uint32_t n, uint32_t j, int li, const line& l) {
+    soa_store2(lines, n, j, li * 6 + 0, l.a);
+    soa_store2(lines, n, j, li * 6 + 2, l.b);
+    soa_store2(lines, n, j, li * 6 + 4, l.c);
 }
-GSV_DI void g2j_store(uint32_t* __restrict__ base, uint32_t n, uint32_t i, const g2j& r) {
-    soa_store2(base, n, i, 0, r.x);
-    soa_store2(base, n, i, 2, r.y);
-    soa_store2(base, n, i, 4, r.z);
-    soa_store2(base, n, i, 6, r.t);
-}
-// pts: [P.x, P.y, Q.x.x, Q.x.y, Q.y.x, Q.y.y] x 9 words per pair
-GSV_DI g1a pts_load_p(const uint32_t* __restrict__ pts, uint32_t n, uint32_t j) {
-    return g1a{soa_load(pts, n, j, 0), soa_load(pts, n, j, 1)};
-}
-GSV_DI g2a pts_load_q(const uint32_t* __restrict__ pts, uint32_t n, uint32_t j) {
-    return g2a{soa_load2(pts, n, j, 2), soa_load2(pts, n, j, 4)};
+GSV_DI line line_load(const uint32_t* __restrict__ lines, uint32_t n, uint32_t j, int li) {
+    return line{soa_load2(lines, n, j, li * 6 + 0), soa_load2(lines, n, j, li * 6 + 2), soa_load2(lines, n, j, li * 6 + 4)};
 }
 
 // gfP.Unmarshal (gfp.go:61-78) + montEncode: big-endian bytes -> Montgomery form (R = 2^261);
@@ -544,13 +544,43 @@ GSV_DI void fp_marshal(uint8_t* out, const fq& a) {
 // ---------------------------------------------------------------- kernels
 enum : uint8_t { PS_OK = 0, PS_SKIP = 1, PS_BAD = 2 };
 
-// Two waves per SIMD: simple VALU ops issue at twice the rate with a second wave
-// (profiles/r01_microbench_lat.txt), and a full batch has 4 waves of pairs per SIMD.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_bn_prepare(const uint8_t* __restrict__ in,
+// The lines of one pair (optate.go:122-210 for affine Q and P, neither at infinity: the loop's
+// doubling / addition steps and the two Frobenius additions), in the order the Miller loop
+// multiplies them in.  Lines of an invalid or infinite pair are computed but never used.
+GSV_DI void pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j, const g1a& P, const g2a& Q) {
+    g2j r{Q.x, Q.y, fp2_one(), fp2_one()};
+    fp2 r2 = s2(fp2_sqr(Q.y));
+    g2a mQ{Q.x, s2(fp2_neg(Q.y))};
+    int li = 0;
+#pragma unroll 1
+    for (int i = 64; i > 0; i--) {
+        line_store(lines, npairs, j, li++, line_double_i(r, P));
+        uint64_t bit = 1ull << (i - 1);
+        if ((NAF_POS | NAF_NEG) & bit) line_store(lines, npairs, j, li++, line_add_i(r, (NAF_POS & bit) ? Q : mQ, P, r2));
+    }
+    // Q1 = pi(Q), -Q2 = -pi^2(Q) (optate.go:168-209)
+    g2a q1{s2(fp2_mul(fp2_conj(Q.x), fp2_const(FQ_XI_P1_3_X, FQ_XI_P1_3_Y))),
+           s2(fp2_mul(fp2_conj(Q.y), fp2_const(FQ_XI_P1_2_X, FQ_XI_P1_2_Y)))};
+    g2a mq2{s2(fp2_mul_fp(Q.x, fq_const(FQ_XI_PSQ1_3))), Q.y};
+    line_store(lines, npairs, j, li++, line_add_i(r, q1, P, s2(fp2_sqr(q1.y))));
+    line_store(lines, npairs, j, li, line_add_i(r, mq2, P, s2(fp2_sqr(mq2.y))));
+}
+
+// Blocks [0, nb) are role 0 (checks), blocks [nb, 2 nb) role 1 (lines) of the same 64 pairs: the
+// roles are whole waves, so they run side by side on different SIMDs without divergence.
+// BN_PREP_WAVES waves per SIMD (a register budget of 512 / BN_PREP_WAVES): simple VALU ops issue at
+// twice the rate with a second wave (profiles/r01_microbench_lat.txt), against the spills of a
+// 256-register budget.
+#ifndef BN_PREP_WAVES
+#define BN_PREP_WAVES 2
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVES))) void k_bn_prepare(const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ pair_src,
                                                    uint32_t npairs, uint8_t* __restrict__ pstat,
-                                                   uint32_t* __restrict__ pts /* [54 words][npairs] */) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                   uint32_t* __restrict__ lines /* [91 * 54 words][npairs] */) {
+    uint32_t nb = (npairs + 63) / 64;
+    bool role_lines = blockIdx.x >= nb;
+    uint32_t i = (role_lines ? blockIdx.x - nb : blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= npairs) return;
     const uint8_t* s = in + pair_src[i];
     g1a P;
@@ -561,16 +591,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     ok = fp_unmarshal(Q.x.y, s + 96) && ok;
     ok = fp_unmarshal(Q.y.x, s + 128) && ok;
     ok = fp_unmarshal(Q.y.y, s + 160) && ok;
+    if (role_lines) {
+        pair_lines(lines, npairs, i, P, Q);
+        return;
+    }
     bool inf1 = fq_is_zero(P.x) && fq_is_zero(P.y);
     bool inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
     if (ok && !inf1)  // curve.go:39-52: y^2 == x^3 + 3
         ok = fq_eq(fq_mul(P.y, P.y), fq_add(fq_mul(fq_mul(P.x, P.x), P.x), fq_const(FQ_THREE)));
     if (ok && !inf2) ok = g2_in_subgroup(&Q);
     pstat[i] = !ok ? PS_BAD : (inf1 || inf2) ? PS_SKIP : PS_OK;
-    soa_store(pts, npairs, i, 0, P.x);
-    soa_store(pts, npairs, i, 1, P.y);
-    soa_store2(pts, npairs, i, 2, Q.x);
-    soa_store2(pts, npairs, i, 4, Q.y);
 }
 
 // ---- per-check multi-Miller loop.  The product of a check's Miller values equals one loop that
@@ -584,10 +614,12 @@ enum : uint8_t { CS_OK = 0, CS_BAD = 1, CS_ONE = 2 };  // CS_ONE: no finite pair
 // A lane runs the loop over a group of <= k of its check's pairs (k = 4 covers a whole 4-pair check;
 // smaller k when the batch is too small to give every SIMD work — the host's choice), and k_bn_final
 // multiplies a check's lane values: the same exact product, so the same verdict.
-__global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ lane_first, uint32_t nlanes,
+#ifndef BN_MILLER_WAVES
+#define BN_MILLER_WAVES 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WAVES))) void k_bn_miller(const uint32_t* __restrict__ lane_first, uint32_t nlanes,
                                                   const uint32_t* __restrict__ pidx, const uint8_t* __restrict__ pstat,
-                                                  const uint32_t* __restrict__ pts, uint32_t npairs,
-                                                  uint32_t* __restrict__ rs /* [72 words][npairs] */,
+                                                  const uint32_t* __restrict__ lines, uint32_t npairs,
                                                   uint8_t* __restrict__ cstat,
                                                   uint32_t* __restrict__ fv /* [108 words][nlanes] */) {
     uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -595,61 +627,34 @@ __global__ __launch_bounds__(64) void k_bn_miller(const uint32_t* __restrict__ l
     uint32_t b = lane_first[c], e = lane_first[c + 1];
     bool bad = false, any = false;
     for (uint32_t q = b; q < e; q++) {
-        uint32_t j = pidx[q];
-        uint8_t st = pstat[j];
+        uint8_t st = pstat[pidx[q]];
         bad = bad || st == PS_BAD;
-        if (st != PS_OK) continue;
-        any = true;
-        g2a Q = pts_load_q(pts, npairs, j);
-        g2j_store(rs, npairs, j, g2j{Q.x, Q.y, fp2_one(), fp2_one()});
+        any = any || st == PS_OK;
     }
     cstat[c] = bad ? CS_BAD : any ? CS_OK : CS_ONE;
     if (bad || !any) return;
     fp12 f = fp12_one();
-    // The loop body is inlined down to the out-of-line F_p products, so f, R and the line stay in
-    // registers.  R and P are (re)loaded per line and R stored before the line product, so only f
-    // and the line are live across mul_line (the R reload hits L2).
+    int li = 0;
 #pragma unroll 1
     for (int i = 64; i > 0; i--) {
         if (i != 64) f = fp12_sqr_i(f);
         uint64_t bit = 1ull << (i - 1);
-        bool add = ((NAF_POS | NAF_NEG) & bit) != 0;
+        int nl = ((NAF_POS | NAF_NEG) & bit) ? 2 : 1;
 #pragma unroll 1
         for (uint32_t q = b; q < e; q++) {
             uint32_t j = pidx[q];
             if (pstat[j] != PS_OK) continue;
 #pragma unroll 1
-            for (int k = 0; k < (add ? 2 : 1); k++) {
-                g1a P = pts_load_p(pts, npairs, j);
-                g2j r = g2j_load(rs, npairs, j);
-                line l;
-                if (k == 0) {
-                    l = line_double_i(r, P);
-                } else {  // Q is only needed on the NAF's nonzero digits
-                    g2a Q = pts_load_q(pts, npairs, j);
-                    fp2 r2 = s2(fp2_sqr(Q.y));
-                    if (NAF_NEG & bit) Q.y = s2(fp2_neg(Q.y));
-                    l = line_add_i(r, Q, P, r2);
-                }
-                g2j_store(rs, npairs, j, r);
-                mul_line_i(f, l);
-            }
+            for (int k = 0; k < nl; k++) mul_line_i(f, line_load(lines, npairs, j, li + k));
         }
+        li += nl;
     }
-    // Q1 = pi(Q), -Q2 = -pi^2(Q) (optate.go:168-209), per pair
+#pragma unroll 1
     for (uint32_t q = b; q < e; q++) {
         uint32_t j = pidx[q];
         if (pstat[j] != PS_OK) continue;
-        g1a P = pts_load_p(pts, npairs, j);
-        g2a A = pts_load_q(pts, npairs, j);
-        g2j r = g2j_load(rs, npairs, j);
-        g2a q1{s2(fp2_mul(fp2_conj(A.x), fp2_const(FQ_XI_P1_3_X, FQ_XI_P1_3_Y))),
-               s2(fp2_mul(fp2_conj(A.y), fp2_const(FQ_XI_P1_2_X, FQ_XI_P1_2_Y)))};
-        g2a mq2{s2(fp2_mul_fp(A.x, fq_const(FQ_XI_PSQ1_3))), A.y};
-        line l = line_add_i(r, q1, P, s2(fp2_sqr(q1.y)));
-        mul_line_p(&f, &l);
-        l = line_add_i(r, mq2, P, s2(fp2_sqr(mq2.y)));
-        mul_line_p(&f, &l);
+#pragma unroll 1
+        for (int k = 0; k < 2; k++) mul_line_i(f, line_load(lines, npairs, j, li + k));
     }
     fp12_store(fv, nlanes, c, f);
 }
@@ -865,13 +870,13 @@ hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, u
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
-                                uint8_t* d_pstat, uint32_t* d_pts, uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv,
+                                uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
                                 uint8_t* d_verdict, bool final3, hipStream_t st, void (*timer_begin)(void*, int),
                                 void (*timer_end)(void*, int), void* tctx) {
     if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        hipLaunchKernelGGL(bn::k_bn_prepare, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                           d_pstat, d_pts);
+        hipLaunchKernelGGL(bn::k_bn_prepare, dim3(2 * ((npairs + 63) / 64)), dim3(64), 0, st, d_in, d_pair_src,
+                           npairs, d_pstat, d_lines);
         if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -879,7 +884,7 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
     if (nchecks) {
         if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
         hipLaunchKernelGGL(bn::k_bn_miller, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
-                           d_pidx, d_pstat, d_pts, npairs, d_rs, d_lstat, d_fv);
+                           d_pidx, d_pstat, d_lines, npairs, d_lstat, d_fv);
         if (timer_end) timer_end(tctx, GSV_K_PAIRING);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -75,7 +75,7 @@ struct Shape {
     // SK_PAIRING
     size_t np = 0, nl = 0, nchecks = 0;
     bool final3 = false;
-    size_t o_src = 0, o_pidx = 0, o_lfirst = 0, o_clane = 0, o_cbad = 0, o_pstat = 0, o_pts = 0, o_rs = 0,
+    size_t o_src = 0, o_pidx = 0, o_lfirst = 0, o_clane = 0, o_cbad = 0, o_pstat = 0, o_lines = 0,
            o_lstat = 0, o_fv = 0;
     // SK_NOTARY
     uint32_t max_txs = 0, sfx_len = 0;
@@ -796,8 +796,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.o_clane = L.add((n + 1) * 4);
     s.o_cbad = L.add(n);
     s.o_pstat = L.add(np + 1);
-    s.o_pts = L.add(np * 54 * 4 + 4);
-    s.o_rs = L.add(np * 72 * 4 + 4);
+    s.o_lines = L.add(np * 91 * 54 * 4 + 4);  // the pairs' Miller-loop lines (bn256.hip BN_NLINES)
     s.o_lstat = L.add(s.nl + 1);
     s.o_fv = L.add(s.nl * 108 * 4 + 4);
     s.stage(s.o_src, pair_src.data(), np);
@@ -811,7 +810,7 @@ int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verd
     return hip_err(gsv::launch_bn256_pairing(
         d_in, s.at<uint64_t>(s.o_src), (uint32_t)s.np, s.at<uint32_t>(s.o_lfirst), s.at<uint32_t>(s.o_pidx),
         (uint32_t)s.nl, s.at<uint32_t>(s.o_clane), s.at<uint8_t>(s.o_cbad), (uint32_t)s.nchecks,
-        s.at<uint8_t>(s.o_pstat), s.at<uint32_t>(s.o_pts), s.at<uint32_t>(s.o_rs), s.at<uint8_t>(s.o_lstat),
+        s.at<uint8_t>(s.o_pstat), s.at<uint32_t>(s.o_lines), s.at<uint8_t>(s.o_lstat),
         s.at<uint32_t>(s.o_fv), d_verdict, s.final3, st, hook_begin, hook_end, c));
 }
 

@@ -52,13 +52,13 @@ hipError_t launch_header_verify(const uint8_t* d_sid32, const uint8_t* d_root32,
 // offset of pair p in d_in.  A check's pairs are split into Miller lanes of <= k pairs each: lane l
 // runs the multi-Miller loop over pidx[lane_first[l] .. lane_first[l+1]), check c owns lanes
 // [check_lane[c], check_lane[c+1]); cbad[c] != 0 marks a ragged input length (no pairs, verdict
-// BAD_INPUT).  Workspaces (F_p elements are 9 words, bn254_fe9.cuh): pstat[npairs], pts[54][npairs],
-// rs[72][npairs], lstat[nlanes], fv[108][nlanes] words.  final3: the final exponentiation runs on three cooperating lanes per check
+// BAD_INPUT).  Workspaces (F_p elements are 9 words, bn254_fe9.cuh): pstat[npairs],
+// lines[91 * 54][npairs], lstat[nlanes], fv[108][nlanes] words.  final3: the final exponentiation runs on three cooperating lanes per check
 // (small batches)
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
-                                uint8_t* d_pstat, uint32_t* d_pts, uint32_t* d_rs, uint8_t* d_lstat, uint32_t* d_fv,
+                                uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
                                 uint8_t* d_verdict, bool final3, hipStream_t st, void (*timer_begin)(void*, int),
                                 void (*timer_end)(void*, int), void* tctx);
 
