@@ -51,6 +51,24 @@ template <class T>
 GSV_DI fp2 s2(const T& a) { return fp2_store(a); }
 GSV_DI fq fq_c(const uint32_t c[9]) { return fq_store(fq_const(c)); }
 
+// F_p^6 products of the F_p^12 routines: inline, or (BN_FP6_OOL) one out-of-line copy per operand
+// type pair, operands by pointer — a third of the code of an inlined F_p^12 product in the I-cache
+#ifndef BN_FP6_OOL
+#define BN_FP6_OOL 0
+#endif
+template <class A, class B, class R>
+static BN_NI void fp6_mul_ool(R* e, const fp6t<A>* a, const fp6t<B>* b) { *e = fp6_mul(*a, *b); }
+template <class A, class B>
+GSV_DI auto fp6_mulx(const fp6t<A>& a, const fp6t<B>& b) {
+#if BN_FP6_OOL
+    decltype(fp6_mul(a, b)) r;
+    fp6_mul_ool(&r, &a, &b);
+    return r;
+#else
+    return fp6_mul(a, b);
+#endif
+}
+
 // ---------------------------------------------------------------- F_p^12 (gfp12.go)
 GSV_DI fp12 fp12_one() { return fp12{fp6_zero(), fp6_one()}; }
 // IsOne (gfp12.go:34-37) on canonical residues: y.z.y == R mod p (one), everything else zero
@@ -85,9 +103,9 @@ GSV_DI fp12 fp12_frob_p2(const fp12& a) {
 // gfp12.go:94-106.  Karatsuba over F_p^6: x = (a.x + a.y)(b.x + b.y) - a.x b.x - a.y b.y equals the
 // reference's a.x b.y + b.x a.y (3 F_p^6 products instead of 4, the same field element).
 GSV_DI fp12 fp12_mul_i(const fp12& a, const fp12& b) {
-    auto v0 = fp6_mul(a.x, b.x);
-    auto v1 = fp6_mul(a.y, b.y);
-    fp6 tx = fp6_store(fp6_sub(fp6_sub(fp6_mul(fp6_add(a.x, a.y), fp6_add(b.x, b.y)), v0), v1));
+    auto v0 = fp6_mulx(a.x, b.x);
+    auto v1 = fp6_mulx(a.y, b.y);
+    fp6 tx = fp6_store(fp6_sub(fp6_sub(fp6_mulx(fp6_add(a.x, a.y), fp6_add(b.x, b.y)), v0), v1));
     return fp12{tx, fp6_store(fp6_add(v1, fp6_mul_tau(v0)))};
 }
 static BN_NI void fp12_mul_p(fp12* pe, const fp12* pa, const fp12* pb) { *pe = fp12_mul_i(*pa, *pb); }
@@ -98,9 +116,9 @@ GSV_DI fp12 fp12_mul(const fp12& a, const fp12& b) {
 }
 // gfp12.go:129-143
 GSV_DI fp12 fp12_sqr_i(const fp12& a) {
-    fp6 v0 = fp6_store(fp6_mul(a.x, a.y));
+    fp6 v0 = fp6_store(fp6_mulx(a.x, a.y));
     auto t = fp6_add(fp6_mul_tau(a.x), a.y);
-    fp6 ty = fp6_store(fp6_sub(fp6_sub(fp6_mul(fp6_add(a.x, a.y), t), v0), fp6_mul_tau(v0)));
+    fp6 ty = fp6_store(fp6_sub(fp6_sub(fp6_mulx(fp6_add(a.x, a.y), t), v0), fp6_mul_tau(v0)));
     return fp12{fp6_store(fp6_add(v0, v0)), ty};
 }
 // Squaring in the cyclotomic subgroup (Granger-Scott, "Faster squaring in the cyclotomic subgroup of
@@ -109,23 +127,34 @@ GSV_DI fp12 fp12_sqr_i(const fp12& a) {
 // (optate.go:218-222) — and it yields the same field element as fp12_sqr there.  Coefficients of
 // a = sum c_k w^k over F_p^2 (w^2 = tau, tau^3 = xi): c0 = y.z, c1 = x.z, c2 = y.y, c3 = x.y,
 // c4 = y.x, c5 = x.x.  One coefficient pair (p, q) gives sq = p^2 xi + q^2 and tc = 2 p q.
+// The inputs are reduced once (value < 3p), so every product below has a tiny output bound and
+// only the outputs c0', c2', c4' (and c1' after its xi factor) need a reduction when stored.
 struct cyc_pair { fp2 lo, hi; };
+using fp2r = fp2m<1, 3>;
+template <int L, int V>
+GSV_DI fp2r fp2_reduce(const fp2m<L, V>& a) { return fp2r{fq_reduce(a.x), fq_reduce(a.y)}; }
+// 2 p q by two dual products: x = 2(px qy + py qx), y = 2(py qy - px qx)
+GSV_DI auto fp2_mul2x(const fp2r& p, const fp2r& q) {
+    auto px2 = fq_add(p.x, p.x), py2 = fq_add(p.y, p.y);
+    return fp2_of(fq_dot(px2, q.y, py2, q.x), fq_dot(py2, q.y, px2, fq_neg(q.x)));
+}
 template <bool XI_TC>
-GSV_DI cyc_pair cyclo_pair(const fp2& p, const fp2& q, const fp2& m1, const fp2& m2) {
-    auto tp = fp2_sqr(p);
-    auto tq = fp2_sqr(q);
-    auto tc = fp2_sub(fp2_sub(fp2_sqr(fp2_add(p, q)), tp), tq);  // 2 p q
-    fp2 sq = s2(fp2_add(fp2_mul_xi(tp), tq));                    // p^2 xi + q^2
-    fp2 tcx;
-    if constexpr (XI_TC) tcx = s2(fp2_mul_xi(tc));
-    else tcx = s2(tc);
-    // lo = 3 sq - 2 m1, hi = 3 tc + 2 m2
-    auto lo = fp2_add(fp2_dbl(fp2_sub(sq, m1)), sq);
-    auto hi = fp2_add(fp2_dbl(fp2_add(tcx, m2)), tcx);
-    return cyc_pair{s2(lo), s2(hi)};
+GSV_DI cyc_pair cyclo_pair(const fp2r& p, const fp2r& q, const fp2r& m1, const fp2r& m2) {
+    auto sq = fp2_add(fp2_mul_xi(fp2_sqr(p)), fp2_sqr(q));  // p^2 xi + q^2
+    auto tc = fp2_mul2x(p, q);                               // 2 p q
+    cyc_pair r;
+    r.lo = s2(fp2_add(fp2_dbl(fp2_sub(sq, m1)), sq));        // 3 sq - 2 m1
+    if constexpr (XI_TC) {
+        auto tcx = fp2_mul_xi(tc);
+        r.hi = s2(fp2_add(fp2_dbl(fp2_add(tcx, m2)), tcx));  // 3 xi tc + 2 m2
+    } else {
+        r.hi = s2(fp2_add(fp2_dbl(fp2_add(tc, m2)), tc));    // 3 tc + 2 m2
+    }
+    return r;
 }
 GSV_DI fp12 fp12_cyclo_sqr_i(const fp12& a) {
-    const fp2 &x0 = a.y.z, &x1 = a.y.y, &x2 = a.y.x, &x3 = a.x.z, &x4 = a.x.y, &x5 = a.x.x;
+    fp2r x0 = fp2_reduce(a.y.z), x1 = fp2_reduce(a.y.y), x2 = fp2_reduce(a.y.x);
+    fp2r x3 = fp2_reduce(a.x.z), x4 = fp2_reduce(a.x.y), x5 = fp2_reduce(a.x.x);
     cyc_pair r0 = cyclo_pair<false>(x4, x0, x0, x4);  // c0', c3'
     cyc_pair r1 = cyclo_pair<false>(x2, x3, x1, x5);  // c2', c5'
     cyc_pair r2 = cyclo_pair<true>(x5, x1, x2, x3);   // c4', c1'
@@ -193,15 +222,13 @@ GSV_DI void gather3(T out[3], const T& mine, int base) {  // out[r] = lane (base
 static BN_NI void fp12_cyclo_sqr3(fp12* pe, const fp12* pa, int role, int base) {
     const fp12 a = *pa;
     const fp2 &x0 = a.y.z, &x1 = a.y.y, &x2 = a.y.x, &x3 = a.x.z, &x4 = a.x.y, &x5 = a.x.x;
-    fp2 p = role == 0 ? x4 : role == 1 ? x2 : x5;
-    fp2 q = role == 0 ? x0 : role == 1 ? x3 : x1;
-    fp2 m1 = role == 0 ? x0 : role == 1 ? x1 : x2;
-    fp2 m2 = role == 0 ? x4 : role == 1 ? x5 : x3;
+    fp2r p = fp2_reduce(role == 0 ? x4 : role == 1 ? x2 : x5);
+    fp2r q = fp2_reduce(role == 0 ? x0 : role == 1 ? x3 : x1);
+    fp2r m1 = fp2_reduce(role == 0 ? x0 : role == 1 ? x1 : x2);
+    fp2r m2 = fp2_reduce(role == 0 ? x4 : role == 1 ? x5 : x3);
     // the xi factor on tc only for role 2, as a select after the shared formula
-    auto tp = fp2_sqr(p);
-    auto tq = fp2_sqr(q);
-    fp2 tc = s2(fp2_sub(fp2_sub(fp2_sqr(fp2_add(p, q)), tp), tq));
-    fp2 sq = s2(fp2_add(fp2_mul_xi(tp), tq));
+    auto sq = fp2_add(fp2_mul_xi(fp2_sqr(p)), fp2_sqr(q));
+    fp2 tc = s2(fp2_mul2x(p, q));
     fp2 tcx = s2(fp2_mul_xi(tc));
     if (role == 2) tc = tcx;
     cyc_pair mine, all[3];
@@ -428,40 +455,38 @@ static BN_NI void final_exp(fp12* out, const fp12* in, int role, int base) {
         else fp12_cyclo_sqr_p(&e, &a);
         return e;
     };
-    fp12 t1 = fp12_conj(*in), t2, fu, fu2, fu3;
+    // the reference's sequence of products, ordered so that at most six F_p^12 values are live
+    // (they sit in per-lane scratch between the out-of-line calls)
+    fp12 t1 = fp12_conj(*in), t2;
     fp12_inv_p(&t2, in);
     t1 = MUL(t1, t2);
-    t2 = fp12_frob_p2(t1);
-    t1 = MUL(t1, t2);
+    t1 = MUL(t1, fp12_frob_p2(t1));
+    fp12 y0;  // frob(t1) frob_p2(t1) frob(frob_p2(t1))
+    {
+        fp12 f2 = fp12_frob_p2(t1);
+        y0 = MUL(MUL(fp12_frob(t1), f2), fp12_frob(f2));
+    }
+    fp12 fu, fu2, fu3;
     if (base >= 0) {
         fp12_exp_u3(&fu, &t1, role, base);
         fp12_exp_u3(&fu2, &fu, role, base);
-        fp12_exp_u3(&fu3, &fu2, role, base);
     } else {
         fp12_exp_u(&fu, &t1);
         fp12_exp_u(&fu2, &fu);
-        fp12_exp_u(&fu3, &fu2);
     }
-    fp12 fp1 = fp12_frob(t1);
-    fp12 fp2_ = fp12_frob_p2(t1);
-    fp12 fp3 = fp12_frob(fp2_);
     fp12 y3 = fp12_conj(fp12_frob(fu));
-    fp12 fu2p = fp12_frob(fu2);
-    fp12 fu3p = fp12_frob(fu3);
-    fp12 y2 = fp12_frob_p2(fu2);
-    fp12 y0 = MUL(MUL(fp1, fp2_), fp3);
-    fp12 y1 = fp12_conj(t1);
+    fp12 y4 = fp12_conj(MUL(fu, fp12_frob(fu2)));
+    if (base >= 0) fp12_exp_u3(&fu3, &fu2, role, base);
+    else fp12_exp_u(&fu3, &fu2);
+    fp12 y6 = fp12_conj(MUL(fu3, fp12_frob(fu3)));
     fp12 y5 = fp12_conj(fu2);
-    fp12 y4 = fp12_conj(MUL(fu, fu2p));
-    fp12 y6 = fp12_conj(MUL(fu3, fu3p));
     fp12 t0 = MUL(MUL(CSQR(y6), y4), y5);
-    t1 = MUL(MUL(y3, y5), t0);
-    t0 = MUL(t0, y2);
-    t1 = MUL(CSQR(t1), t0);
-    t1 = CSQR(t1);
-    t0 = MUL(t1, y1);
-    t1 = MUL(t1, y0);
-    *out = MUL(CSQR(t0), t1);
+    t2 = MUL(MUL(y3, y5), t0);
+    t0 = MUL(t0, fp12_frob_p2(fu2));  // y2
+    t2 = CSQR(MUL(CSQR(t2), t0));
+    t0 = MUL(t2, fp12_conj(t1));      // y1
+    t2 = MUL(t2, y0);
+    *out = MUL(CSQR(t0), t2);
 }
 
 // ---------------------------------------------------------------- SoA helpers
