@@ -35,7 +35,8 @@ def build():
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(HERE, "liboracle.so")
+        # GSV_ORACLE_LIB: another build of the same sources (tools/sanitize.sh: ASan/UBSan)
+        path = os.environ.get("GSV_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)

@@ -17,6 +17,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built libgsv.so")
 
 
+# extra flags for the host builds of device headers / host decoders (tests/native): set by
+# tools/sanitize.sh, which also preloads the ASan/UBSan runtimes into the Python process
+SANITIZE_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                  "-fno-sanitize-recover=undefined"] if os.environ.get("GSV_SANITIZE") == "1" else []
+
+
+def build_native(src, out, std="c++17"):
+    """g++ -shared of tests/native/<src> (plus the sanitizer flags when GSV_SANITIZE=1)."""
+    import subprocess
+    subprocess.run(["g++", "-O2", f"-std={std}", "-shared", "-fPIC", "-Wno-unknown-pragmas"] + SANITIZE_FLAGS +
+                   ["-o", str(out), os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", src)],
+                   check=True)
+    import ctypes
+    return ctypes.CDLL(str(out))
+
+
 def golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)

@@ -24,10 +24,8 @@ I2 = ctypes.c_int * 2
 
 @pytest.fixture(scope="module")
 def lib(tmp_path_factory):
-    out = tmp_path_factory.mktemp("bn9") / "bn9_host.so"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-o", str(out),
-                    os.path.join(HERE, "native", "bn9_host.cpp")], check=True)
-    return ctypes.CDLL(str(out))
+    from conftest import build_native
+    return build_native("bn9_host.cpp", tmp_path_factory.mktemp("bn9") / "bn9_host.so")
 
 
 def val(l):

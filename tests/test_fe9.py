@@ -20,10 +20,8 @@ U9 = ctypes.c_uint32 * 9
 
 @pytest.fixture(scope="module")
 def lib(tmp_path_factory):
-    out = tmp_path_factory.mktemp("fe9") / "fe9_host.so"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-o", str(out),
-                    os.path.join(HERE, "native", "fe9_host.cpp")], check=True)
-    return ctypes.CDLL(str(out))
+    from conftest import build_native
+    return build_native("fe9_host.cpp", tmp_path_factory.mktemp("fe9") / "fe9_host.so")
 
 
 def val(l):
