@@ -324,6 +324,7 @@ FQ_FN auto fq_mul(const fqm<La, Va>& a, const fqm<Lb, Vb>& b) {
         else return fq_mul(a, fq_normalize(b));
     } else {
         GSV_OPC(gsv::OPC_BN_MUL);
+        GSV_OPC(gsv::OPC_BN_REDC);
         fqm<1, fq_prod_v(Va, Vb)> r;
 #if defined(__HIPCC__) && !BN_MUL_INLINE
         fqv o = fq_mul_v(fq_tov(a), fq_tov(b));
@@ -350,6 +351,7 @@ FQ_FN auto fq_mul2(const fqm<La, Va>& a, const fqm<Lb, Vb>& b, const fqm<Lc, Vc>
     } else {
         GSV_OPC(gsv::OPC_BN_MUL);
         GSV_OPC(gsv::OPC_BN_MUL);
+        GSV_OPC(gsv::OPC_BN_REDC);
         fqm<1, (Va * Vb + Vc * Vd) / 168 + 2> r;
 #if defined(__HIPCC__) && !BN_MUL_INLINE
         fqv o = fq_mul2_v(fq_tov(a), fq_tov(b), fq_tov(c), fq_tov(d));
@@ -420,6 +422,7 @@ FQ_FN auto fq_dot(const T&... xs) {
             B[t][i] = p[2 * t + 1][i];
         }
     }
+    GSV_OPC(gsv::OPC_BN_REDC);
     fqm<1, S / 168 + 2> r;
     fq_redc_n<N>(r.v, A, B);
     return r;

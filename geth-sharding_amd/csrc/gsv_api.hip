@@ -8,6 +8,7 @@
 // matching gsv_*_prepare call (which may allocate and synchronize) and cached per context, keyed by
 // exactly those host-side arguments.  A *_dev call whose shape was not prepared returns
 // GSV_E_NOT_PREPARED without touching the device.
+#include <rccl/rccl.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -138,6 +139,9 @@ struct gsv_ctx {
     std::list<std::unique_ptr<Shape>> shapes;
     size_t shape_bytes = 0;
     std::mutex smu;  // shapes, cur_stream / cur_capture
+    // RCCL communicator of the shard partition (gsv_comm_init), nullptr = single rank
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
 };
 
 namespace {
@@ -456,6 +460,7 @@ void gsv_ctx_destroy(gsv_ctx* c) {
     drain_timing(c);
     for (auto e : c->free_events) hipEventDestroy(e);
     c->shapes.clear();
+    if (c->comm) ncclCommDestroy(c->comm);
     if (c->arena) hipFree(c->arena);
     if (c->gtab) hipFree(c->gtab);
     hipStreamDestroy(c->stream);
@@ -1347,6 +1352,132 @@ int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t
     HIPCHK(hipStreamSynchronize(c->stream));
     for (size_t i = 0; i < n_shards; i++)
         if (ntx_out[i] > max_txs) return GSV_E_TOO_LARGE;
+    return GSV_SUCCESS;
+}
+
+// ------------------------------------------------------------------ shard partition + RCCL all-gather
+// Record per shard (the layout of gsv/shards.py): root 32 | ntx 4 | bitmap ceil(max_txs/8), padded to
+// 8 bytes.  Each rank packs its block's records with three strided copies, one ncclAllGather moves
+// every rank's block (ceil(S/N) records, the tail of a short block unused), and three strided copies
+// per rank unpack the gathered records into shard order.
+int gsv_comm_unique_id(uint8_t id[GSV_COMM_ID_BYTES]) {
+    if (!id) return GSV_E_INVALID_ARG;
+    static_assert(sizeof(ncclUniqueId) == GSV_COMM_ID_BYTES, "RCCL unique id size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return GSV_E_RCCL;
+    memcpy(id, &u, sizeof(u));
+    return GSV_SUCCESS;
+}
+
+int gsv_comm_init(gsv_ctx* c, const uint8_t id[GSV_COMM_ID_BYTES], int nranks, int rank) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    if (c->comm) {
+        ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) {
+        c->comm = nullptr;
+        return GSV_E_RCCL;
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    return GSV_SUCCESS;
+}
+
+int gsv_comm_info(gsv_ctx* c, int* nranks, int* rank) {
+    if (!c) return GSV_E_INVALID_ARG;
+    if (nranks) *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+    return GSV_SUCCESS;
+}
+
+int gsv_shard_range(size_t n_shards, int nranks, int rank, size_t* first, size_t* count) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || !first || !count) return GSV_E_INVALID_ARG;
+    size_t a = n_shards * (size_t)rank / (size_t)nranks, b = n_shards * (size_t)(rank + 1) / (size_t)nranks;
+    *first = a;
+    *count = b - a;
+    return GSV_SUCCESS;
+}
+
+int gsv_notary_validate_partition(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n_total,
+                                  const uint8_t* chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
+                                  uint8_t* root32_all, uint32_t* ntx_all, uint8_t* bitmap_all,
+                                  uint8_t* senders_out, uint8_t* status_out) {
+    if (!c || !off || (n_total && (!root32_all || !ntx_all || !bitmap_all))) return GSV_E_INVALID_ARG;
+    const int N = c->nranks, r = c->rank;
+    size_t first = 0, n = 0;
+    gsv_shard_range(n_total, N, r, &first, &n);
+    int rc = notary_args(chain_id, chain_id_len, signer_kind, n_total, max_txs);
+    if (rc || n_total == 0) return rc;
+    if (n && !bodies) return GSV_E_INVALID_ARG;
+    for (size_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_BODY) return GSV_E_TOO_LARGE;
+    const size_t bm = (max_txs + 7) / 8, R = (36 + bm + 7) / 8 * 8, per = (n_total + N - 1) / N;
+    const size_t nt = n * (size_t)max_txs;
+    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g2(c->smu);
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint64_t> st, en;
+    uint64_t pos = n ? stage_offsets(off, n, st, en) : 0;
+    size_t staged = al(pos + 16) + al(n * 32 + 1) + al(n * 4 + 1) + al(n * bm + 1) + al(nt * 20 + 1) + al(nt + 1) +
+                    al(per * R) + al((size_t)N * per * R);
+    Shape s;
+    if (n) {
+        rc = shape_temp(c, staged,
+                        [&](Shape& ns, Layout& L) {
+                            return notary_shape(c, ns, st.data(), en.data(), n, chain_id, chain_id_len, signer_kind,
+                                                max_txs, L);
+                        },
+                        s);
+    } else {
+        rc = arena_reserve(c, staged);
+    }
+    if (rc) return rc;
+    Carve cv(c->arena);
+    uint8_t* d_b = cv.take<uint8_t>(pos + 16);
+    uint8_t* d_r = cv.take<uint8_t>(n * 32 + 1);
+    uint32_t* d_n = cv.take<uint32_t>(n * 4 + 1);
+    uint8_t* d_bm = cv.take<uint8_t>(n * bm + 1);
+    uint8_t* d_snd = cv.take<uint8_t>(nt * 20 + 1);
+    uint8_t* d_st = cv.take<uint8_t>(nt + 1);
+    uint8_t* d_rec = cv.take<uint8_t>(per * R);
+    uint8_t* d_all = cv.take<uint8_t>((size_t)N * per * R);
+    hipStream_t sm = c->stream;
+    HIPCHK(hipMemsetAsync(d_rec, 0, per * R, sm));
+    if (n) {
+        rc = stage_bodies(c, d_b, bodies, off, n, st, en);
+        if (rc) return rc;
+        rc = shape_run(c, s, sm, [&] {
+            return notary_run(c, s, n, d_b, d_r, d_n, d_bm, senders_out ? d_snd : nullptr, status_out ? d_st : nullptr, sm);
+        });
+        if (rc) return rc;
+        HIPCHK(hipMemcpy2DAsync(d_rec, R, d_r, 32, 32, n, hipMemcpyDeviceToDevice, sm));
+        HIPCHK(hipMemcpy2DAsync(d_rec + 32, R, d_n, 4, 4, n, hipMemcpyDeviceToDevice, sm));
+        HIPCHK(hipMemcpy2DAsync(d_rec + 36, R, d_bm, bm, bm, n, hipMemcpyDeviceToDevice, sm));
+    }
+    if (N > 1 && c->comm) {
+        if (ncclAllGather(d_rec, d_all, per * R, ncclUint8, c->comm, sm) != ncclSuccess) return GSV_E_RCCL;
+    } else {
+        HIPCHK(hipMemcpyAsync(d_all, d_rec, per * R, hipMemcpyDeviceToDevice, sm));
+    }
+    for (int q = 0; q < N; q++) {
+        size_t f = 0, k = 0;
+        gsv_shard_range(n_total, N, q, &f, &k);
+        if (!k) continue;
+        const uint8_t* src = d_all + (size_t)q * per * R;
+        HIPCHK(hipMemcpy2DAsync(root32_all + f * 32, 32, src, R, 32, k, hipMemcpyDeviceToHost, sm));
+        HIPCHK(hipMemcpy2DAsync(ntx_all + f, 4, src + 32, R, 4, k, hipMemcpyDeviceToHost, sm));
+        HIPCHK(hipMemcpy2DAsync(bitmap_all + f * bm, bm, src + 36, R, bm, k, hipMemcpyDeviceToHost, sm));
+    }
+    if (n && senders_out) HIPCHK(hipMemcpyAsync(senders_out, d_snd, nt * 20, hipMemcpyDeviceToHost, sm));
+    if (n && status_out) HIPCHK(hipMemcpyAsync(status_out, d_st, nt, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipStreamSynchronize(sm));
+    for (size_t i = 0; i < n_total; i++)
+        if (ntx_all[i] > max_txs) return GSV_E_TOO_LARGE;
     return GSV_SUCCESS;
 }
 

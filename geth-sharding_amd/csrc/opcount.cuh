@@ -12,6 +12,7 @@ enum OpKind : int {
     OPC_SC_SQR = 3,
     OPC_BN_MUL = 4,  // BN254 F_p Montgomery product
     OPC_MODINV = 5,  // safegcd inversion (mod p, mod n, BN254 p)
+    OPC_BN_REDC = 6, // BN254 Montgomery reduction (one per fq_mul / fq_mul2 / fq_dot)
     OPC_N = 8
 };
 }  // namespace gsv

@@ -324,6 +324,55 @@ def _notary_synth_dev(self, seed, shard0, n_shards, txs_per_shard, bodies_t, exp
                                            _tptr(exp_sender_t), sp))
 
 
+def comm_unique_id() -> bytes:
+    """An RCCL unique id (gsv.h gsv_comm_unique_id): rank 0 creates it and sends it to the others."""
+    buf = np.zeros(128, np.uint8)
+    check(_lib.load().gsv_comm_unique_id(_ptr(buf)))
+    return buf.tobytes()
+
+
+def shard_range(n_shards: int, nranks: int, rank: int):
+    """(first, count) of rank's contiguous shard block (gsv.h gsv_shard_range)."""
+    first, count = ctypes.c_size_t(), ctypes.c_size_t()
+    check(_lib.load().gsv_shard_range(n_shards, nranks, rank, ctypes.byref(first), ctypes.byref(count)))
+    return first.value, count.value
+
+
+def _comm_init(self, uid: bytes, nranks: int, rank: int):
+    buf = np.frombuffer(bytes(uid), np.uint8).copy()
+    check(_lib.load().gsv_comm_init(self._h, _ptr(buf), int(nranks), int(rank)))
+
+
+def _comm_info(self):
+    n, r = ctypes.c_int(), ctypes.c_int()
+    check(_lib.load().gsv_comm_info(self._h, ctypes.byref(n), ctypes.byref(r)))
+    return n.value, r.value
+
+
+def _notary_validate_partition(self, my_bodies, n_total: int, chain_id: int = 1,
+                               signer_kind: int = _lib.SIGNER_EIP155, max_txs: int = 8192,
+                               want_senders=False, want_status=False):
+    """gsv.h gsv_notary_validate_partition: this rank's block of bodies in, every shard's record out:
+    (roots (S,32), ntx (S,), bitmap (S, ceil(max_txs/8)), senders | None, status | None) — the last
+    two for this rank's shards only."""
+    n = len(my_bodies)
+    bm = (max_txs + 7) // 8
+    roots = np.zeros((n_total, 32), np.uint8)
+    ntx = np.zeros(n_total, np.uint32)
+    bitmap = np.zeros((n_total, bm), np.uint8)
+    senders = np.zeros((n, max_txs, 20), np.uint8) if want_senders and n else None
+    status = np.zeros((n, max_txs), np.uint8) if want_status and n else None
+    flat, off = _pack(my_bodies) if n else (np.zeros(1, np.uint8), np.zeros(1, np.uint64))
+    cbuf = np.frombuffer(_be(chain_id) + b"\0", np.uint8)
+    check(_lib.load().gsv_notary_validate_partition(self._h, _ptr(flat), _ptr(off), n_total, _ptr(cbuf),
+                                                    len(_be(chain_id)), int(signer_kind), int(max_txs), _ptr(roots),
+                                                    _ptr(ntx), _ptr(bitmap), _ptr(senders), _ptr(status)))
+    return roots, ntx, bitmap, senders, status
+
+
+Context.comm_init = _comm_init
+Context.comm_info = _comm_info
+Context.notary_validate_partition = _notary_validate_partition
 Context.notary_prepare = _notary_prepare
 Context.chunk_root_prepare = _chunk_root_prepare
 Context.pairing_prepare = _pairing_prepare

@@ -107,6 +107,12 @@ SIGNATURES = [
     ("gsv_derive_sha_prepare", ctypes.c_int, [_vp, _vp, _vp, _sz]),
     ("gsv_collation_poc_prepare", ctypes.c_int, [_vp, _vp, _sz, _vp, _sz]),
     ("gsv_collation_header_prepare", ctypes.c_int, [_vp, _sz]),
+    ("gsv_comm_unique_id", ctypes.c_int, [_vp]),
+    ("gsv_comm_init", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
+    ("gsv_comm_info", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    ("gsv_shard_range", ctypes.c_int, [_sz, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
+    ("gsv_notary_validate_partition", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, ctypes.c_int, ctypes.c_uint32,
+                                                     _vp, _vp, _vp, _vp, _vp]),
 ]
 
 _lib = None

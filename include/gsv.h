@@ -288,6 +288,28 @@ int gsv_collation_header_verify_batch_dev(gsv_ctx *ctx, const uint8_t *d_shard_i
                                           uint8_t *d_hash32_out, uint8_t *d_signer20_out, uint8_t *d_status,
                                           void *stream);
 
+/* ---- multi-GPU: the shard partition and its one collective ----
+ * One process per GPU.  Rank r of N owns the contiguous shard block [floor(S r / N), floor(S (r+1) / N))
+ * of S shards (the reference runs one shard per node, --shardid, sharding/node/backend.go:245-284;
+ * S = 100 in the SMC, sharding/contracts/sharding_manager.sol:56).
+ * gsv_comm_unique_id: rank 0 creates the id and hands it to the other ranks (any channel);
+ * gsv_comm_init binds an RCCL communicator (xGMI within the node) to the context's device. */
+#define GSV_COMM_ID_BYTES 128
+int gsv_comm_unique_id(uint8_t id[GSV_COMM_ID_BYTES]);
+int gsv_comm_init(gsv_ctx *ctx, const uint8_t id[GSV_COMM_ID_BYTES], int nranks, int rank);
+int gsv_comm_info(gsv_ctx *ctx, int *nranks, int *rank);
+/* first shard and shard count of `rank`'s block */
+int gsv_shard_range(size_t n_shards, int nranks, int rank, size_t *first, size_t *count);
+/* Validates this rank's block (bodies/off: its `count` shards, as gsv_notary_validate_shards) and
+ * all-gathers the fixed-size per-shard records over RCCL, so every rank returns the records of all
+ * n_total_shards shards in shard order: root32_all[32 S], ntx_all[S], valid_bitmap_all[S ceil(max_txs/8)].
+ * senders_out / status_out (optional) cover this rank's own shards only ([count][max_txs]).
+ * Needs gsv_comm_init (a context without one behaves as N = 1). */
+int gsv_notary_validate_partition(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off, size_t n_total_shards,
+                                  const uint8_t *chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
+                                  uint8_t *root32_all, uint32_t *ntx_all, uint8_t *valid_bitmap_all,
+                                  uint8_t *senders_out, uint8_t *status_out);
+
 #ifdef __cplusplus
 }
 #endif

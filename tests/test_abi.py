@@ -41,3 +41,16 @@ def test_no_oracle_in_product_package():
                 txt = open(os.path.join(dp, f), errors="ignore").read()
                 for bad in ("from oracle", "import oracle", "liboracle", "libgsvref", "oracle_"):
                     assert bad not in txt, (f, bad)
+
+
+def test_shard_range_matches_partition_arithmetic():
+    """gsv_shard_range (pure host arithmetic, callable without a GPU) == gsv/shards.py's blocks"""
+    import gsv
+    from gsv import shards as SH
+    for n in (0, 1, 7, 100, 101):
+        for world in (1, 2, 3, 8):
+            got = [gsv.shard_range(n, world, r) for r in range(world)]
+            want = [(SH.shard_range(r, world, n)[0], SH.shard_range(r, world, n)[1] - SH.shard_range(r, world, n)[0])
+                    for r in range(world)]
+            assert got == want
+            assert sum(c for _, c in got) == n

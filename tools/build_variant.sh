@@ -17,5 +17,5 @@ wait
 for f in gsv_api keccak ecrecover chunk_root tx_host bn256 notary collation; do
     case " $VSRCS " in *" $f "*) ;; *) cp build/$f.o $R/variants/$name/ ;; esac
 done
-/opt/rocm/bin/hipcc -fPIC --offload-arch=gfx950 -shared -o $R/variants/$name/libgsv.so $R/variants/$name/*.o
+/opt/rocm/bin/hipcc -fPIC --offload-arch=gfx950 -shared -o $R/variants/$name/libgsv.so $R/variants/$name/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built $R/variants/$name/libgsv.so
