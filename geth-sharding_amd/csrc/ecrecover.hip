@@ -11,11 +11,12 @@
 //
 // Algorithm (ours, MI355X-first — not libsecp256k1's Strauss-wNAF, which branches per digit and
 // wastes SIMD lanes).  Field arithmetic: 9 x 29-bit limbs with lazy reduction (secp256k1_fe9.cuh).
-//   * u2*R: GLV split u2 = k1 + k2*lambda (|k1|,|k2| < 2^128), fixed-schedule odd-digit w=3
-//     recoding (every 3rd bit adds, identical across the wave: no divergence), 4-entry table
-//     {1,3,5,7}R built on an isomorphic curve (libsecp-style "global z") so all table points are
-//     affine without an inversion, lambda-table x-coordinates precomputed (x * beta).
-//     129 doublings + 88 mixed additions.
+//   * u2*R: GLV split u2 = k1 + k2*lambda (|k1|,|k2| < 2^128), fixed-schedule odd-digit w = 4
+//     recoding (recover_dev.cuh GSV_GLV_W: an add every 4th bit, identical across the wave: no
+//     divergence), 8-entry table {1,3,...,15}R in per-lane scratch, built on an isomorphic curve
+//     (libsecp-style "global z") so all table points are affine without an inversion; the lambda
+//     half uses (beta x, y).  128 doublings + 66 mixed additions (w = 3 with the 4-entry table in
+//     LDS: 129 + 88, measured 6 % slower: 15.5 -> 14.5 ms per 2^20 recoveries).
 //   * u1*G: fixed-base comb, 16 windows of 16 bits from an 80 MiB affine table in HBM (Infinity-Cache
 //     resident, one random 80-byte entry per window, prefetched a window ahead), 16 mixed additions
 //     and no doublings (gsv_internal.h COMB_BITS).

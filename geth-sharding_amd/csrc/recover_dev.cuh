@@ -33,16 +33,26 @@ __device__ constexpr uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75F
 __device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
                                            0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
 
-// LDS table: 72 words per lane, lane-minor ([word][GSV_LTAB_STRIDE]); the kernels that call
-// recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS]
-constexpr int GSV_LTAB_STRIDE = 256;
-constexpr int GSV_LTAB_WORDS = 72 * GSV_LTAB_STRIDE;
-constexpr int GLV_DIGITS = 44;
+// u2 R's GLV halves are recoded into fixed-schedule odd digits of GSV_GLV_W bits: digits in
+// {+-1, +-3, ..., +-(2^W - 1)}, a table of the 2^(W-1) odd multiples of R, W doublings per digit.
+#ifndef GSV_GLV_W
+#define GSV_GLV_W 4
+#endif
+constexpr int GLV_W = GSV_GLV_W;
+constexpr int GLV_NT = 1 << (GLV_W - 1);             // table entries
+constexpr int GLV_DIGITS = (130 + GLV_W - 1) / GLV_W;  // k + skew < 2^129 (the split's bound is 2^128)
+static_assert(GLV_W >= 3 && GLV_W <= 4 && GLV_DIGITS * 4 <= 192, "digits pack 4 bits (sign + 3-bit index) into 6 words");
 // where the per-lane GLV table lives: 0 = LDS ([word][256 lanes] per block), 1 = a private array
 // (scratch: memory only for resident lanes, served by L1/L2)
 #ifndef GSV_GLV_TAB
-#define GSV_GLV_TAB 0
+#define GSV_GLV_TAB (GLV_W == 3 ? 0 : 1)
 #endif
+// LDS table: 18 GLV_NT words per lane, lane-minor ([word][GSV_LTAB_STRIDE]); the kernels that call
+// recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS].  Two waves per
+// SIMD leave room for 72 words a lane (w = 3); a wider window keeps its table in scratch.
+constexpr int GSV_LTAB_STRIDE = 256;
+constexpr int GSV_LTAB_WORDS = 18 * GLV_NT * GSV_LTAB_STRIDE;
+static_assert(GSV_GLV_TAB == 1 || GLV_W == 3, "the LDS table is sized for w = 3 at two waves per SIMD");
 // waves per SIMD the recovery kernels are compiled for (register budget 512 / waves)
 #ifndef GSV_ECR_WAVES
 #define GSV_ECR_WAVES 2
@@ -53,7 +63,7 @@ constexpr int GLV_DIGITS = 44;
 #else
 #define GSV_LTAB_DECL
 #define GSV_LTAB_LANE nullptr
-#endif  // w = 3 odd digits cover k < 2^131 (bound is 2^128)
+#endif
 
 // ---------------------------------------------------------------------------- scalar helpers
 GSV_DI void sc_from_const(sc& r, const uint32_t c[8]) {
@@ -95,9 +105,11 @@ GSV_DI void sc_split_lambda(sc& r1, sc& r2, const sc& k) {
 
 GSV_DI bool sc_is_high(const sc& a) { return limbs_lt(HALF_N, a.v); }
 
-// Fixed-schedule odd-digit recoding, w = 3: k (odd after skew) = sum d_i 8^i with
-// d_i in {+-1,+-3,+-5,+-7}.  Digit i packed in 4 bits: bit 3 = negative, bits 0-1 = (|d|-1)/2.
-GSV_DI void recode_w3(uint32_t dig[6], uint32_t& skew, const sc& kin) {
+// Fixed-schedule odd-digit recoding, w = GLV_W: k (odd after skew) = sum d_i 2^(w i) with
+// d_i odd in [-(2^w - 1), 2^w - 1].  Digit i packed in 4 bits: bit 3 = negative, bits 0-2 = (|d|-1)/2.
+GSV_DI void recode_glv(uint32_t dig[6], uint32_t& skew, const sc& kin) {
+    constexpr uint32_t MASK = (2u << GLV_W) - 1u;
+    constexpr int32_t OFF = 1 << GLV_W;
     uint32_t k[5] = {kin.v[0], kin.v[1], kin.v[2], kin.v[3], kin.v[4]};
     skew = (k[0] & 1u) ^ 1u;
     // k += skew  (k < 2^129 so no overflow out of 5 limbs)
@@ -113,13 +125,13 @@ GSV_DI void recode_w3(uint32_t dig[6], uint32_t& skew, const sc& kin) {
 #pragma unroll
     for (int i = 0; i < GLV_DIGITS; i++) {
         int32_t d;
-        if (i < GLV_DIGITS - 1) d = (int32_t)(k[0] & 15u) - 8;
-        else d = (int32_t)(k[0] & 15u);
+        if (i < GLV_DIGITS - 1) d = (int32_t)(k[0] & MASK) - OFF;
+        else d = (int32_t)(k[0] & MASK);
         uint32_t neg = d < 0 ? 1u : 0u;
         uint32_t mag = (uint32_t)(d < 0 ? -d : d);
         uint32_t code = (neg << 3) | ((mag - 1u) >> 1);
         dig[i >> 3] |= code << ((i & 7) * 4);
-        // k = (k - d) >> 3
+        // k = (k - d) >> w
         int64_t t = (int64_t)k[0] - d;
         uint32_t kk[5];
         kk[0] = (uint32_t)t;
@@ -131,8 +143,8 @@ GSV_DI void recode_w3(uint32_t dig[6], uint32_t& skew, const sc& kin) {
             carry = u >> 32;
         }
 #pragma unroll
-        for (int j = 0; j < 4; j++) k[j] = (kk[j] >> 3) | (kk[j + 1] << 29);
-        k[4] = kk[4] >> 3;
+        for (int j = 0; j < 4; j++) k[j] = (kk[j] >> GLV_W) | (kk[j + 1] << (32 - GLV_W));
+        k[4] = kk[4] >> GLV_W;
     }
 }
 
@@ -316,7 +328,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     sc_neg(u1, u1);
     sc_mul(u2, rn, ss);
 
-    // ---- u2 * R via GLV + fixed w=3 odd digits
+    // ---- u2 * R via GLV + fixed w = GLV_W odd digits
     sc k1, k2;
     sc_split_lambda(k1, k2, u2);
     bool neg1 = sc_is_high(k1), neg2 = sc_is_high(k2);
@@ -330,41 +342,91 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         for (int i = 0; i < 8; i++) k2.v[i] = neg2 ? nk.v[i] : k2.v[i];
     }
     uint32_t dig1[6], dig2[6], skew1, skew2;
-    recode_w3(dig1, skew1, k1);
-    recode_w3(dig2, skew2, k2);
+    recode_glv(dig1, skew1, k1);
+    recode_glv(dig2, skew2, k2);
 
-    ge9 T[4];
-    fe9 zfac;
-    build_r_table9(T, zfac, x, y);
-    // The GLV table lives in LDS (ltab = this lane's column of a [word][256 lanes] array:
-    // conflict-free for any per-lane entry index), not in VGPRs: 72 words {x[4], y[4]} would
-    // otherwise cost the kernel occupancy.  Each add loads its entry by index (no selects);
-    // lambda(P) = (beta x, y) costs one product per lambda add.
+    // The GLV table {x[GLV_NT], y[GLV_NT]} of the odd multiples (2e+1)R lives in LDS (w = 3:
+    // ltab = this lane's column of a [word][256 lanes] array, conflict-free for any per-lane entry
+    // index) or in a private array (wider windows), not in VGPRs, which would cost occupancy.
+    // Each add loads its entry by index (no selects); lambda(P) = (beta x, y) costs one product per
+    // lambda add.
 #if GSV_GLV_TAB == 1
-    uint32_t ptab[72];
+    uint32_t ptab[18 * GLV_NT];
 #define GLV_TAB(i) ptab[i]
 #else
 #define GLV_TAB(i) ltab[(i) * GSV_LTAB_STRIDE]
 #endif
+    constexpr int YO = 9 * GLV_NT;  // y coordinates after the x coordinates
+    // Odd multiples on an isomorphic curve E'' (affine there, no inversion): P_e = (2e+1)R' built
+    // by mixed adds of D = 2R' with their z-ratios zr_e, stored unscaled, then every entry below the
+    // last rescaled to the last one's Z by the product of the later z-ratios.  A Jacobian result
+    // (X, Y, Z) on E'' is (X, Y, Z zfac) on E.
+    fe9 zfac;
+    {
+        gej9 R1;
+        R1.x = x;
+        R1.y = y;
+        fe9_set_u32(R1.z, 1);
+        gej9 D;
+        gej9_dbl(D, R1);
+        fe9 u2, u3;
+        fe9_sqr(u2, D.z);  // 2*2 -> 1
+        fe9_mul(u3, u2, D.z);
+        ge9 Dp;
+        Dp.x = D.x;
+        Dp.y = D.y;
+        gej9 P;
+        fe9_mul(P.x, x, u2);
+        fe9_mul(P.y, y, u3);
+        fe9_set_u32(P.z, 1);
+        fe9 zr[GLV_NT];
 #pragma unroll
-    for (int e = 0; e < 4; e++) {
+        for (int e = 0; e < GLV_NT; e++) {
+            if (e) {
+                gej9 Pn;
+                gej9_add_ge_zr(Pn, zr[e], P, Dp);
+                P = Pn;
+            }
 #pragma unroll
-        for (int k = 0; k < 9; k++) {
-            GLV_TAB(e * 9 + k) = T[e].x.v[k];
-            GLV_TAB(36 + e * 9 + k) = T[e].y.v[k];
+            for (int k = 0; k < 9; k++) {
+                GLV_TAB(e * 9 + k) = P.x.v[k];
+                GLV_TAB(YO + e * 9 + k) = P.y.v[k];
+            }
         }
+        fe9 f = zr[GLV_NT - 1];
+#pragma unroll
+        for (int e = GLV_NT - 2; e >= 0; e--) {
+            fe9 ex, ey;
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                ex.v[k] = GLV_TAB(e * 9 + k);
+                ey.v[k] = GLV_TAB(YO + e * 9 + k);
+            }
+            ge9 q;
+            scale_xy9(q, ex, ey, f);
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                GLV_TAB(e * 9 + k) = q.x.v[k];
+                GLV_TAB(YO + e * 9 + k) = q.y.v[k];
+            }
+            if (e) fe9_mul(f, f, zr[e]);  // 2*2 -> 1
+        }
+        fe9_mul(zfac, D.z, P.z);  // 2*2 -> 1
     }
 
     gej9 acc;
     bool ainf = true;
-    acc.x = T[0].x;
-    acc.y = T[0].y;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        acc.x.v[k] = GLV_TAB(k);
+        acc.y.v[k] = GLV_TAB(YO + k);
+    }
     fe9_set_u32(acc.z, 1);
 #pragma unroll 1
     for (int i = GLV_DIGITS - 1; i >= 0; i--) {
         if (i != GLV_DIGITS - 1) {
 #pragma unroll 1
-            for (int d = 0; d < 3; d++) gej9_dbl(acc, acc);
+            for (int d = 0; d < GLV_W; d++) gej9_dbl(acc, acc);
         }
         uint32_t c1 = (sel_word(dig1, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
         uint32_t c2 = (sel_word(dig2, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
@@ -373,12 +435,12 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         for (int j = 0; j < 2; j++) {
             uint32_t c = j ? c2 : c1;
             bool ng = j ? neg2 : neg1;
-            uint32_t xo = (c & 3u) * 9u;
+            uint32_t xo = (c & (uint32_t)(GLV_NT - 1)) * 9u;
             ge9 P;
 #pragma unroll
             for (int k = 0; k < 9; k++) {
                 P.x.v[k] = GLV_TAB(xo + k);
-                P.y.v[k] = GLV_TAB(36u + xo + k);
+                P.y.v[k] = GLV_TAB((uint32_t)YO + xo + k);
             }
             if (j != 0) {  // wave-uniform
                 fe9 beta;
@@ -397,8 +459,11 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         bool ng = j ? neg2 : neg1;
         uint32_t sk = j ? skew2 : skew1;
         ge9 P;
-        P.x = T[0].x;
-        P.y = T[0].y;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            P.x.v[k] = GLV_TAB(k);
+            P.y.v[k] = GLV_TAB(YO + k);
+        }
         if (j != 0) {
             fe9 beta;
             fe9_from_const(beta, BETA);
