@@ -13,7 +13,8 @@
 // wastes SIMD lanes).  Field arithmetic: 9 x 29-bit limbs with lazy reduction (secp256k1_fe9.cuh).
 //   * u2*R: GLV split u2 = k1 + k2*lambda (|k1|,|k2| < 2^128), fixed-schedule odd-digit w = 4
 //     recoding (recover_dev.cuh GSV_GLV_W: an add every 4th bit, identical across the wave: no
-//     divergence), 8-entry table {1,3,...,15}R in per-lane scratch, built on an isomorphic curve
+//     divergence), 8-entry table {1,3,...,15}R (entries 0..3 in LDS, 4..7 in per-lane scratch: the
+//     LDS of two waves per SIMD holds four), built on an isomorphic curve
 //     (libsecp-style "global z") so all table points are affine without an inversion; the lambda
 //     half uses (beta x, y).  128 doublings + 66 mixed additions (w = 3 with the 4-entry table in
 //     LDS: 129 + 88, measured 6 % slower: 15.5 -> 14.5 ms per 2^20 recoveries).

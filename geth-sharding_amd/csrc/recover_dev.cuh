@@ -43,21 +43,22 @@ constexpr int GLV_NT = 1 << (GLV_W - 1);             // table entries
 constexpr int GLV_DIGITS = (130 + GLV_W - 1) / GLV_W;  // k + skew < 2^129 (the split's bound is 2^128)
 static_assert(GLV_W >= 3 && GLV_W <= 4 && GLV_DIGITS * 4 <= 192, "digits pack 4 bits (sign + 3-bit index) into 6 words");
 // where the per-lane GLV table lives: 0 = LDS ([word][256 lanes] per block), 1 = a private array
-// (scratch: memory only for resident lanes, served by L1/L2)
+// (scratch: memory only for resident lanes, served by L1/L2), 2 = entries 0..3 in LDS and the rest
+// in the private array.  Two waves per SIMD leave LDS room for 72 words a lane: four entries.
 #ifndef GSV_GLV_TAB
-#define GSV_GLV_TAB (GLV_W == 3 ? 0 : 1)
+#define GSV_GLV_TAB (GLV_W == 3 ? 0 : 2)
 #endif
-// LDS table: 18 GLV_NT words per lane, lane-minor ([word][GSV_LTAB_STRIDE]); the kernels that call
-// recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS].  Two waves per
-// SIMD leave room for 72 words a lane (w = 3); a wider window keeps its table in scratch.
+constexpr int GLV_LNT = GSV_GLV_TAB == 1 ? 0 : GSV_GLV_TAB == 2 ? 4 : GLV_NT;  // entries in LDS
+static_assert(GLV_LNT <= 4 && GLV_LNT <= GLV_NT, "LDS holds at most four entries at two waves per SIMD");
+// LDS part: 18 GLV_LNT words per lane, lane-minor ([word][GSV_LTAB_STRIDE]); the kernels that call
+// recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS].
 constexpr int GSV_LTAB_STRIDE = 256;
-constexpr int GSV_LTAB_WORDS = 18 * GLV_NT * GSV_LTAB_STRIDE;
-static_assert(GSV_GLV_TAB == 1 || GLV_W == 3, "the LDS table is sized for w = 3 at two waves per SIMD");
+constexpr int GSV_LTAB_WORDS = 18 * GLV_LNT * GSV_LTAB_STRIDE;
 // waves per SIMD the recovery kernels are compiled for (register budget 512 / waves)
 #ifndef GSV_ECR_WAVES
 #define GSV_ECR_WAVES 2
 #endif
-#if GSV_GLV_TAB == 0
+#if GSV_GLV_TAB != 1
 #define GSV_LTAB_DECL __shared__ uint32_t ltab[GSV_LTAB_WORDS]
 #define GSV_LTAB_LANE (ltab + threadIdx.x)
 #else
@@ -350,13 +351,23 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     // index) or in a private array (wider windows), not in VGPRs, which would cost occupancy.
     // Each add loads its entry by index (no selects); lambda(P) = (beta x, y) costs one product per
     // lambda add.
-#if GSV_GLV_TAB == 1
-    uint32_t ptab[18 * GLV_NT];
-#define GLV_TAB(i) ptab[i]
-#else
-#define GLV_TAB(i) ltab[(i) * GSV_LTAB_STRIDE]
-#endif
-    constexpr int YO = 9 * GLV_NT;  // y coordinates after the x coordinates
+    // entry e < GLV_LNT: LDS words [e*9 + k] (x) and [9*GLV_LNT + e*9 + k] (y); the others: the
+    // private array, x at [(e - GLV_LNT)*9 + k], y after all x
+    constexpr int PNT = GLV_NT - GLV_LNT;
+    uint32_t ptab[18 * (PNT > 0 ? PNT : 1)];
+#define GLV_L(i) ltab[(i) * GSV_LTAB_STRIDE]
+#define GLV_X(e, k) ((e) < GLV_LNT ? GLV_L((e) * 9 + (k)) : ptab[((e) - GLV_LNT) * 9 + (k)])
+#define GLV_Y(e, k) ((e) < GLV_LNT ? GLV_L(9 * GLV_LNT + (e) * 9 + (k)) : ptab[9 * PNT + ((e) - GLV_LNT) * 9 + (k)])
+#define GLV_SET(e, k, X, Y)                                           \
+    do {                                                              \
+        if ((e) < GLV_LNT) {                                          \
+            GLV_L((e) * 9 + (k)) = (X);                               \
+            GLV_L(9 * GLV_LNT + (e) * 9 + (k)) = (Y);                 \
+        } else {                                                      \
+            ptab[((e) - GLV_LNT) * 9 + (k)] = (X);                    \
+            ptab[9 * PNT + ((e) - GLV_LNT) * 9 + (k)] = (Y);          \
+        }                                                             \
+    } while (0)
     // Odd multiples on an isomorphic curve E'' (affine there, no inversion): P_e = (2e+1)R' built
     // by mixed adds of D = 2R' with their z-ratios zr_e, stored unscaled, then every entry below the
     // last rescaled to the last one's Z by the product of the later z-ratios.  A Jacobian result
@@ -388,10 +399,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
                 P = Pn;
             }
 #pragma unroll
-            for (int k = 0; k < 9; k++) {
-                GLV_TAB(e * 9 + k) = P.x.v[k];
-                GLV_TAB(YO + e * 9 + k) = P.y.v[k];
-            }
+            for (int k = 0; k < 9; k++) GLV_SET(e, k, P.x.v[k], P.y.v[k]);
         }
         fe9 f = zr[GLV_NT - 1];
 #pragma unroll
@@ -399,16 +407,13 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             fe9 ex, ey;
 #pragma unroll
             for (int k = 0; k < 9; k++) {
-                ex.v[k] = GLV_TAB(e * 9 + k);
-                ey.v[k] = GLV_TAB(YO + e * 9 + k);
+                ex.v[k] = GLV_X(e, k);
+                ey.v[k] = GLV_Y(e, k);
             }
             ge9 q;
             scale_xy9(q, ex, ey, f);
 #pragma unroll
-            for (int k = 0; k < 9; k++) {
-                GLV_TAB(e * 9 + k) = q.x.v[k];
-                GLV_TAB(YO + e * 9 + k) = q.y.v[k];
-            }
+            for (int k = 0; k < 9; k++) GLV_SET(e, k, q.x.v[k], q.y.v[k]);
             if (e) fe9_mul(f, f, zr[e]);  // 2*2 -> 1
         }
         fe9_mul(zfac, D.z, P.z);  // 2*2 -> 1
@@ -418,8 +423,8 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     bool ainf = true;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
-        acc.x.v[k] = GLV_TAB(k);
-        acc.y.v[k] = GLV_TAB(YO + k);
+        acc.x.v[k] = GLV_X(0, k);
+        acc.y.v[k] = GLV_Y(0, k);
     }
     fe9_set_u32(acc.z, 1);
 #pragma unroll 1
@@ -435,12 +440,22 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         for (int j = 0; j < 2; j++) {
             uint32_t c = j ? c2 : c1;
             bool ng = j ? neg2 : neg1;
-            uint32_t xo = (c & (uint32_t)(GLV_NT - 1)) * 9u;
+            uint32_t ei = c & (uint32_t)(GLV_NT - 1);
             ge9 P;
+            if (GLV_LNT == GLV_NT || (GLV_LNT > 0 && ei < (uint32_t)GLV_LNT)) {
+                uint32_t xo = ei * 9u;
 #pragma unroll
-            for (int k = 0; k < 9; k++) {
-                P.x.v[k] = GLV_TAB(xo + k);
-                P.y.v[k] = GLV_TAB((uint32_t)YO + xo + k);
+                for (int k = 0; k < 9; k++) {
+                    P.x.v[k] = GLV_L(xo + k);
+                    P.y.v[k] = GLV_L(9u * GLV_LNT + xo + k);
+                }
+            } else {  // the lanes whose digit indexes the private part (divergent: each side loads only its lanes)
+                uint32_t xo = (ei - (uint32_t)GLV_LNT) * 9u;
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    P.x.v[k] = ptab[xo + k];
+                    P.y.v[k] = ptab[9u * PNT + xo + k];
+                }
             }
             if (j != 0) {  // wave-uniform
                 fe9 beta;
@@ -461,8 +476,8 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         ge9 P;
 #pragma unroll
         for (int k = 0; k < 9; k++) {
-            P.x.v[k] = GLV_TAB(k);
-            P.y.v[k] = GLV_TAB(YO + k);
+            P.x.v[k] = GLV_X(0, k);
+            P.y.v[k] = GLV_Y(0, k);
         }
         if (j != 0) {
             fe9 beta;
