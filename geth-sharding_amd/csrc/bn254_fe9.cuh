@@ -48,7 +48,10 @@ namespace bn {
 constexpr uint32_t FQ_M29 = 0x1FFFFFFFu;
 constexpr int FQ_LMAX = 8;    // limbs <= 8 (2^29 - 1) < 2^32
 constexpr int FQ_VMAX = 160;  // value < 160 p: limb 8 of a normalised element stays < 2^29
-constexpr int VS = 32;        // value bound of a stored element
+#ifndef BN_VS
+#define BN_VS 20
+#endif
+constexpr int VS = BN_VS;     // value bound of a stored element
 
 template <int L, int V>
 struct fqm {

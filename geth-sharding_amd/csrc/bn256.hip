@@ -591,22 +591,9 @@ GSV_DI void pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j
     line_store(lines, npairs, j, li, line_add_i(r, mq2, P, s2(fp2_sqr(mq2.y))));
 }
 
-// Blocks [0, nb) are role 0 (checks), blocks [nb, 2 nb) role 1 (lines) of the same 64 pairs: the
-// roles are whole waves, so they run side by side on different SIMDs without divergence.
-// BN_PREP_WAVES waves per SIMD (a register budget of 512 / BN_PREP_WAVES): simple VALU ops issue at
-// twice the rate with a second wave (profiles/r01_microbench_lat.txt), against the spills of a
-// 256-register budget.
-#ifndef BN_PREP_WAVES
-#define BN_PREP_WAVES 2
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVES))) void k_bn_prepare(const uint8_t* __restrict__ in,
-                                                   const uint64_t* __restrict__ pair_src,
-                                                   uint32_t npairs, uint8_t* __restrict__ pstat,
-                                                   uint32_t* __restrict__ lines /* [91 * 54 words][npairs] */) {
-    uint32_t nb = (npairs + 63) / 64;
-    bool role_lines = blockIdx.x >= nb;
-    uint32_t i = (role_lines ? blockIdx.x - nb : blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= npairs) return;
+// role 0 (checks) / role 1 (lines) of pair i
+GSV_DI void prepare_pair(bool role_lines, uint32_t i, const uint8_t* __restrict__ in, const uint64_t* __restrict__ pair_src,
+                         uint32_t npairs, uint8_t* __restrict__ pstat, uint32_t* __restrict__ lines) {
     const uint8_t* s = in + pair_src[i];
     g1a P;
     g2a Q;
@@ -626,6 +613,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVE
         ok = fq_eq(fq_mul(P.y, P.y), fq_add(fq_mul(fq_mul(P.x, P.x), P.x), fq_const(FQ_THREE)));
     if (ok && !inf2) ok = g2_in_subgroup(&Q);
     pstat[i] = !ok ? PS_BAD : (inf1 || inf2) ? PS_SKIP : PS_OK;
+}
+
+// Blocks [0, nb) are role 0 (checks), blocks [nb, 2 nb) role 1 (lines) of the same 64 pairs: the
+// roles are whole waves, so they run side by side on different SIMDs without divergence.
+// BN_PREP_WAVES waves per SIMD (a register budget of 512 / BN_PREP_WAVES): simple VALU ops issue at
+// twice the rate with a second wave (profiles/r01_microbench_lat.txt), against the spills of a
+// 256-register budget.
+#ifndef BN_PREP_WAVES
+#define BN_PREP_WAVES 2
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVES))) void k_bn_prepare(const uint8_t* __restrict__ in,
+                                                   const uint64_t* __restrict__ pair_src,
+                                                   uint32_t npairs, uint8_t* __restrict__ pstat,
+                                                   uint32_t* __restrict__ lines /* [91 * 54 words][npairs] */) {
+    uint32_t nb = (npairs + 63) / 64;
+    bool role_lines = blockIdx.x >= nb;
+    uint32_t i = (role_lines ? blockIdx.x - nb : blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    prepare_pair(role_lines, i, in, pair_src, npairs, pstat, lines);
+}
+// BN_PREP_SPLIT: the two roles as separate kernels, each with its own register budget (A/B)
+#ifndef BN_PREP_SPLIT
+#define BN_PREP_SPLIT 0
+#endif
+#ifndef BN_LINES_WAVES
+#define BN_LINES_WAVES 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVES))) void k_bn_check(const uint8_t* __restrict__ in,
+                                                   const uint64_t* __restrict__ pair_src,
+                                                   uint32_t npairs, uint8_t* __restrict__ pstat) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < npairs) prepare_pair(false, i, in, pair_src, npairs, pstat, nullptr);
+}
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_LINES_WAVES))) void k_bn_lines(const uint8_t* __restrict__ in,
+                                                   const uint64_t* __restrict__ pair_src,
+                                                   uint32_t npairs, uint32_t* __restrict__ lines) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, nullptr, lines);
 }
 
 // ---- per-check multi-Miller loop.  The product of a check's Miller values equals one loop that
@@ -900,8 +925,15 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                                 void (*timer_end)(void*, int), void* tctx) {
     if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        hipLaunchKernelGGL(bn::k_bn_prepare, dim3(2 * ((npairs + 63) / 64)), dim3(64), 0, st, d_in, d_pair_src,
-                           npairs, d_pstat, d_lines);
+        if (BN_PREP_SPLIT) {
+            hipLaunchKernelGGL(bn::k_bn_check, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
+                               d_pstat);
+            hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
+                               d_lines);
+        } else {
+            hipLaunchKernelGGL(bn::k_bn_prepare, dim3(2 * ((npairs + 63) / 64)), dim3(64), 0, st, d_in, d_pair_src,
+                               npairs, d_pstat, d_lines);
+        }
         if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
