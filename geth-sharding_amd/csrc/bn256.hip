@@ -709,6 +709,120 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
     fp12_store(fv, nlanes, c, f);
 }
 
+// ---- two-lane Miller step, for batches too small to give every SIMD a wave: lanes (2c, 2c+1) run
+// Miller lane c together.  Both hold the whole accumulator; each F_p^12 squaring's two F_p^6
+// products and each line product's two sparse products (plus half of its F_p^2-scalar product)
+// are split by the lane's role (one instruction stream: the operands are selected, not branched on)
+// and exchanged with ds_bpermute, so the dependent chain per step is about half as long.  Every part
+// computes the same formula as the one-lane routine: the same field elements.
+template <class E, class F>
+GSV_DI auto sel6(bool r, const fp6t<E>& a, const fp6t<F>& b) {  // r ? b : a, at their common bound
+    auto w = fp6_of(a.x, a.y, a.z);
+    auto v = fp6_of(b.x, b.y, b.z);
+    constexpr int l = imax(fp2_traits<decltype(w.x)>::l, fp2_traits<decltype(v.x)>::l);
+    constexpr int vv = imax(fp2_traits<decltype(w.x)>::v, fp2_traits<decltype(v.x)>::v);
+    fp6t<fp2m<l, vv>> o, bw;
+    o = fp6t<fp2m<l, vv>>{fp2_widen<l, vv>(w.x), fp2_widen<l, vv>(w.y), fp2_widen<l, vv>(w.z)};
+    bw = fp6t<fp2m<l, vv>>{fp2_widen<l, vv>(v.x), fp2_widen<l, vv>(v.y), fp2_widen<l, vv>(v.z)};
+    uint32_t* po = (uint32_t*)&o;
+    const uint32_t* pb = (const uint32_t*)&bw;
+#pragma unroll
+    for (int k = 0; k < 54; k++) po[k] = r ? pb[k] : po[k];
+    return o;
+}
+template <int L1, int V1, int L2, int V2>
+GSV_DI auto sel2(bool r, const fp2m<L1, V1>& a, const fp2m<L2, V2>& b) {
+    constexpr int l = imax(L1, L2), v = imax(V1, V2);
+    fp2m<l, v> o = fp2_widen<l, v>(a), bw = fp2_widen<l, v>(b);
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        o.x.v[k] = r ? bw.x.v[k] : o.x.v[k];
+        o.y.v[k] = r ? bw.y.v[k] : o.y.v[k];
+    }
+    return o;
+}
+template <class T>
+GSV_DI void gather2(T out[2], const T& mine, int base) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized");
+    const uint32_t* m = (const uint32_t*)&mine;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        uint32_t* o = (uint32_t*)&out[r];
+#pragma unroll
+        for (int w = 0; w < (int)(sizeof(T) / 4); w++) o[w] = bperm(m[w], base + r);
+    }
+}
+// fp12_sqr_i: role 0 v0 = x y, role 1 (x + y)(tau x + y)
+GSV_DI fp12 fp12_sqr2(const fp12& a, bool role, int base) {
+    auto sum = fp6_add(a.x, a.y);
+    auto t = fp6_add(fp6_mul_tau(a.x), a.y);
+    auto prod = fp6_mul(sel6(role, a.x, sum), sel6(role, a.y, t));
+    decltype(prod) v[2];
+    gather2(v, prod, base);
+    fp6 v0 = fp6_store(v[0]);
+    return fp12{fp6_store(fp6_add(v0, v0)), fp6_store(fp6_sub(fp6_sub(v[1], v0), fp6_mul_tau(v0)))};
+}
+// mul_line_i: role 0 a2 = ret.x (a tau + b) and t3.x, t3.y; role 1 (ret.x + ret.y)(a tau + b + c) and t3.z
+struct line2_part {
+    fp6 q;
+    fp2 t0, t1;
+};
+GSV_DI void mul_line2(fp12& ret, const line& l, bool role, int base) {
+    auto s = fp6_add(ret.x, ret.y);
+    line2_part mine, all[2];
+    mine.q = fp6_store(fp6_mul_sparse(sel6(role, ret.x, s), l.a, sel2(role, l.b, fp2_add(l.b, l.c))));
+    mine.t0 = s2(fp2_mul(sel2(role, ret.y.x, ret.y.z), l.c));
+    mine.t1 = s2(fp2_mul(ret.y.y, l.c));
+    gather2(all, mine, base);
+    fp6 t3{all[0].t0, all[0].t1, all[1].t0};
+    const fp6& a2 = all[0].q;
+    ret.x = fp6_store(fp6_sub(fp6_sub(all[1].q, a2), t3));
+    ret.y = fp6_store(fp6_add(t3, fp6_mul_tau(a2)));
+}
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WAVES))) void k_bn_miller2(
+    const uint32_t* __restrict__ lane_first, uint32_t nlanes, const uint32_t* __restrict__ pidx,
+    const uint8_t* __restrict__ pstat, const uint32_t* __restrict__ lines, uint32_t npairs,
+    uint8_t* __restrict__ cstat, uint32_t* __restrict__ fv) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t c = t >> 1;
+    bool role = (t & 1u) != 0;
+    int base = (int)(threadIdx.x & ~1u);
+    if (c >= nlanes) return;  // both lanes of a pair leave together (nlanes counts pairs of lanes)
+    uint32_t b = lane_first[c], e = lane_first[c + 1];
+    bool bad = false, any = false;
+    for (uint32_t q = b; q < e; q++) {
+        uint8_t st = pstat[pidx[q]];
+        bad = bad || st == PS_BAD;
+        any = any || st == PS_OK;
+    }
+    if (!role) cstat[c] = bad ? CS_BAD : any ? CS_OK : CS_ONE;
+    if (bad || !any) return;
+    fp12 f = fp12_one();
+    int li = 0;
+#pragma unroll 1
+    for (int i = 64; i > 0; i--) {
+        if (i != 64) f = fp12_sqr2(f, role, base);
+        uint64_t bit = 1ull << (i - 1);
+        int nl = ((NAF_POS | NAF_NEG) & bit) ? 2 : 1;
+#pragma unroll 1
+        for (uint32_t q = b; q < e; q++) {
+            uint32_t j = pidx[q];
+            if (pstat[j] != PS_OK) continue;
+#pragma unroll 1
+            for (int k = 0; k < nl; k++) mul_line2(f, line_load(lines, npairs, j, li + k), role, base);
+        }
+        li += nl;
+    }
+#pragma unroll 1
+    for (uint32_t q = b; q < e; q++) {
+        uint32_t j = pidx[q];
+        if (pstat[j] != PS_OK) continue;
+#pragma unroll 1
+        for (int k = 0; k < 2; k++) mul_line2(f, line_load(lines, npairs, j, li + k), role, base);
+    }
+    if (!role) fp12_store(fv, nlanes, c, f);
+}
+
 // role/base as final_exp: the verdict is written by role 0
 // cbad[c] != 0: the check's input length is not a multiple of 192 (errBadPairingInput,
 // core/vm/contracts.go:336-338); it has no pairs
@@ -921,7 +1035,7 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
                                 uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
-                                uint8_t* d_verdict, bool final3, hipStream_t st, void (*timer_begin)(void*, int),
+                                uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
                                 void (*timer_end)(void*, int), void* tctx) {
     if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
@@ -940,13 +1054,17 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
     }
     if (nchecks) {
         if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
-        hipLaunchKernelGGL(bn::k_bn_miller, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
-                           d_pidx, d_pstat, d_lines, npairs, d_lstat, d_fv);
+        if (layout & GSV_BN_LAYOUT_MILLER2)
+            hipLaunchKernelGGL(bn::k_bn_miller2, dim3((2 * nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
+                               d_pidx, d_pstat, d_lines, npairs, d_lstat, d_fv);
+        else
+            hipLaunchKernelGGL(bn::k_bn_miller, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
+                               d_pidx, d_pstat, d_lines, npairs, d_lstat, d_fv);
         if (timer_end) timer_end(tctx, GSV_K_PAIRING);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
-        if (final3)
+        if (layout & GSV_BN_LAYOUT_FINAL3)
             hipLaunchKernelGGL(bn::k_bn_final3, dim3((nchecks + bn::FINAL3_PER_WAVE - 1) / bn::FINAL3_PER_WAVE),
                                dim3(64), 0, st, d_check_lane, nchecks, d_cbad, d_lstat, d_fv, nlanes, d_verdict);
         else

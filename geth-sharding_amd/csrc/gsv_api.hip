@@ -75,7 +75,7 @@ struct Shape {
     ChunkLaunch chunk;  // SK_CHUNK, SK_NOTARY, SK_POC
     // SK_PAIRING
     size_t np = 0, nl = 0, nchecks = 0;
-    bool final3 = false;
+    int layout = 0;  // GSV_BN_LAYOUT_* flags
     size_t o_src = 0, o_pidx = 0, o_lfirst = 0, o_clane = 0, o_cbad = 0, o_pstat = 0, o_lines = 0,
            o_lstat = 0, o_fv = 0;
     // SK_NOTARY
@@ -707,6 +707,12 @@ bool bn_final3(size_t nchecks, int cus) {
     if (const char* e = getenv("GSV_BN_FINAL3")) return atoi(e) != 0;
     return nchecks < (size_t)std::max(cus, 1) * 4 * 64;
 }
+// Two lanes per Miller lane while twice the Miller lanes still fit one wave per SIMD (the Miller
+// kernel's register budget admits one wave per SIMD).  GSV_BN_MILLER2 = 0/1 forces the choice.
+bool bn_miller2(size_t nlanes, int cus) {
+    if (const char* e = getenv("GSV_BN_MILLER2")) return atoi(e) != 0;
+    return 2 * nlanes <= (size_t)std::max(cus, 1) * 4 * 64;
+}
 // Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
 // lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
 // and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
@@ -731,7 +737,8 @@ int device_cus(int device) {
 std::vector<uint64_t> pairing_key(const uint64_t* h_off, size_t n) {
     const char* k = getenv("GSV_BN_PAIRS_PER_LANE");
     const char* f = getenv("GSV_BN_FINAL3");
-    std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0};
+    const char* m = getenv("GSV_BN_MILLER2");
+    std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0, m ? (uint64_t)atoi(m) + 1 : 0};
     key.insert(key.end(), h_off, h_off + n + 1);
     return key;
 }
@@ -794,7 +801,8 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.np = np;
     s.nl = lane_first.size() - 1;
     s.nchecks = n;
-    s.final3 = bn_final3(n, cus);
+    s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
+               (bn_miller2(s.nl, cus) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0);
     s.o_src = L.add(np * 8 + 8);
     s.o_pidx = L.add(np * 4 + 4);
     s.o_lfirst = L.add((s.nl + 1) * 4);
@@ -816,7 +824,7 @@ int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verd
         d_in, s.at<uint64_t>(s.o_src), (uint32_t)s.np, s.at<uint32_t>(s.o_lfirst), s.at<uint32_t>(s.o_pidx),
         (uint32_t)s.nl, s.at<uint32_t>(s.o_clane), s.at<uint8_t>(s.o_cbad), (uint32_t)s.nchecks,
         s.at<uint8_t>(s.o_pstat), s.at<uint32_t>(s.o_lines), s.at<uint8_t>(s.o_lstat),
-        s.at<uint32_t>(s.o_fv), d_verdict, s.final3, st, hook_begin, hook_end, c));
+        s.at<uint32_t>(s.o_fv), d_verdict, s.layout, st, hook_begin, hook_end, c));
 }
 
 // ---- notary: key = chain id, signer, max_txs, body offsets
