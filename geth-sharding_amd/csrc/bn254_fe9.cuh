@@ -45,6 +45,11 @@ namespace bn {
 
 #include "bn9_consts.inc"
 
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(BN_NO_ASM)
+#include "bn9_asm.cuh"
+#define BN9_ASM 1
+#endif
+
 constexpr uint32_t FQ_M29 = 0x1FFFFFFFu;
 constexpr int FQ_LMAX = 8;    // limbs <= 8 (2^29 - 1) < 2^32
 constexpr int FQ_VMAX = 160;  // value < 160 p: limb 8 of a normalised element stays < 2^29
@@ -243,6 +248,28 @@ FQ_FN void fq_cmov(fqm<L, V>& r, const fqm<L, V>& a, bool f) {
 template <bool DUAL>
 FQ_FN void fq_redc_core(uint32_t r[9], const uint32_t a[9], const uint32_t b[9], const uint32_t c[9],
                         const uint32_t d[9]) {
+#if defined(BN9_ASM)
+    if constexpr (DUAL) {
+        uint32_t A[2][9], B[2][9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            A[0][i] = a[i];
+            A[1][i] = c[i];
+            B[0][i] = b[i];
+            B[1][i] = d[i];
+        }
+        fq_redc_asm<2>(r, A, B);
+    } else {
+        uint32_t A[1][9], B[1][9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            A[0][i] = a[i];
+            B[0][i] = b[i];
+        }
+        fq_redc_asm<1>(r, A, B);
+    }
+    return;
+#endif
     uint32_t m[9];
     uint64_t acc = 0;
 #pragma unroll
@@ -372,6 +399,10 @@ FQ_FN auto fq_mul2(const fqm<La, Va>& a, const fqm<Lb, Vb>& b, const fqm<Lc, Vc>
 // (three F_p^2 products each), so it needs 6 reductions instead of 12 and no intermediate additions.
 template <int N>
 FQ_FN void fq_redc_n(uint32_t r[9], const uint32_t (&a)[N][9], const uint32_t (&b)[N][9]) {
+#if defined(BN9_ASM)
+    fq_redc_asm<N>(r, a, b);
+    return;
+#endif
     uint32_t m[9];
     uint64_t acc = 0;
 #pragma unroll

@@ -1,51 +1,111 @@
-"""Generates geth-sharding_amd/csrc/fe9_asm.cuh: the 9 x 29-bit column products of
-secp256k1_fe9.cuh (fe9_mul / fe9_sqr) as ONE inline-asm statement each.
+"""Generates geth-sharding_amd/csrc/fe9_asm.cuh: secp256k1_fe9.cuh's fe9_mul / fe9_sqr (9 x 29-bit
+column product + the 2^261 == 2^37 + 31264 fold of fe9_reduce) as ONE inline-asm statement each.
 
 Why asm.  Written as C++ (`acc += (uint64_t)a[i] * b[j]` per term, `acc >>= 29` per column),
 LLVM re-associates each column's sum into a v_mad_u64_u32 chain that starts at 0 and adds the
-incoming carry with a separate v_lshl_add_u64 (17 extra 64-bit VALU ops per product).  Pinning
-the order with an empty asm after every multiply-add removes those, but hipcc then pads one
-wait state (s_nop 0) after every asm boundary whose output the next VALU reads: 73 s_nop per
-product.  One statement for the whole product has neither: column k's accumulator starts as
-the previous column shifted right by 29 (v_lshrrev_b64) and takes its products as one chain.
+incoming carry with a separate v_lshl_add_u64 (17 extra 64-bit VALU ops per product, 8 more in
+the reduction).  Pinning the order with an empty asm after every multiply-add removes those, but
+hipcc then pads a wait state (s_nop 0) after every asm boundary whose output the next VALU reads:
+73 per product.  One statement for the whole operation has neither: column k's accumulator
+starts as the previous column shifted right by 29 (v_lshrrev_b64) and takes its products as one
+chain; the reduction's running value keeps its carry in a register pair whose high word is 0.
 
-Outputs are the 17 column accumulators as 64-bit register pairs; the caller masks the low
-29 bits of each (a plain v_and_b32 on the low register, which inline asm cannot name) and
-takes the final carry as c[16] >> 29.  Operand numbering: %0..%16 columns, %17 the dead
-carry-out SGPR pair of every v_mad_u64_u32, then the inputs."""
+Inline asm cannot name the low half of a 64-bit operand, so the two running pairs live in fixed,
+clobbered VGPRs (v[2:3], v[4:5]) and the 29-bit limbs are read from their low registers.
+full_lines() is also executed instruction by instruction by tests/test_asm_emulated.py."""
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "geth-sharding_amd", "csrc", "fe9_asm.cuh")
 
 
-def product(terms_of_column, n_inputs_names):
-    """terms_of_column(k) -> list of (input index x, input index y); returns asm text lines."""
-    lines = []
-    for k in range(17):
-        terms = terms_of_column(k)
-        first = True
-        if k > 0:
-            lines.append(f"v_lshrrev_b64 %{k}, 29, %{k - 1}")
-            first = False
-        for (x, y) in terms:
-            src2 = "0" if first else f"%{k}"
-            lines.append(f"v_mad_u64_u32 %{k}, %17, %{18 + x}, %{18 + y}, {src2}")
-            first = False
-    return lines
-
-
-def emit(name, doc, lines, inputs):
-    outs = ", ".join(f'"=&v"(c[{k}])' for k in range(17)) + ', "=&s"(sd)'
-    ins = ", ".join(f'"v"({x})' for x in inputs)
-    body = "\\n\\t".join(lines)
+def full(name, doc, terms_of_column):
+    L = full_lines(terms_of_column)
+    outs = ", ".join([f'"=&v"(r[{i}])' for i in range(9)] + [f'"=&v"(hi[{i}])' for i in range(8)] + ['"=&s"(sd)'])
+    ins = ", ".join([f'"v"(a[{i}])' for i in range(9)] + [f'"v"(b[{j}])' for j in range(9)] +
+                    ['"s"(k31264)', '"s"(k256)', '"s"(k977)'])
+    body = "\\n\\t".join(L)
     return [f"// {doc}",
-            f"__device__ __forceinline__ void {name}(uint64_t c[17], const uint32_t a[9], const uint32_t b[9]) {{",
+            f"__device__ __forceinline__ void {name}(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {{",
+            "    uint32_t hi[8];",
             "    uint64_t sd;",
+            "    uint32_t k31264 = 31264u, k256 = 256u, k977 = 977u;",
             f'    asm("{body}"',
             f"        : {outs}",
-            f"        : {ins});",
+            f"        : {ins}",
+            '        : "v2", "v3", "v4", "v5");',
             "}"]
+
+
+MUL_TERMS = lambda k: [(i, 9 + (k - i)) for i in range(9) if 0 <= k - i < 9]
+
+
+def SQR_TERMS(k):
+    """squaring: b holds the doubled limbs 2 a[j]; cross terms a[i] * 2a[j] (i < j) + a[k/2]^2"""
+    t = [(i, 9 + (k - i)) for i in range(9) if i < k - i < 9]
+    if k % 2 == 0 and k // 2 < 9:
+        t.append((k // 2, k // 2))
+    return t
+
+
+def full_lines(terms_of_column):
+    """Product + reduction (secp256k1_fe9.cuh fe9_reduce restated) in one statement.  Operands:
+    %0..%8 r (o_0..o_8 in place), %9..%16 o_9..o_16, %17 sd, %18..%26 a, %27..%35 b,
+    %36 31264, %37 256, %38 977 (SGPRs).  Fixed pairs: C = v[2:3] (columns, then o17, then T),
+    D = v[4:5] (the reduction's running value)."""
+    C, c0, c1 = "v[2:3]", "v2", "v3"
+    D, d0, d1 = "v[4:5]", "v4", "v5"
+    o = lambda k: f"%{k}" if k < 9 else f"%{k}"
+    a = lambda i: f"%{18 + i}"
+    b = lambda j: f"%{27 + j}"
+    K31264, K256, K977, SD = "%36", "%37", "%38", "%17"
+    L = []
+    for k in range(17):
+        first = True
+        if k > 0:
+            L.append(f"v_lshrrev_b64 {C}, 29, {C}")
+            first = False
+        for (x, y) in terms_of_column(k):
+            xa = a(x)
+            yb = b(y - 9) if y >= 9 else a(y)
+            L.append(f"v_mad_u64_u32 {C}, {SD}, {xa}, {yb}, {'0' if first else C}")
+            first = False
+        L.append(f"v_and_b32_e32 {o(k)}, 0x1fffffff, {c0}")
+    L.append(f"v_lshrrev_b64 {C}, 29, {C}")               # o17 < 2^35
+    # limbs 0..7: c = o_j + carry + 31264 o_{j+9} + 256 o_{j+8}
+    L.append(f"v_mov_b32 {d1}, 0")
+    L.append(f"v_mov_b32 {d0}, {o(0)}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {o(9)}, {K31264}, {D}")
+    L.append(f"v_and_b32_e32 {o(0)}, 0x1fffffff, {d0}")
+    for j in range(1, 8):
+        L.append(f"v_lshrrev_b64 {D}, 29, {D}")           # carry < 2^16: the high word is 0
+        L.append(f"v_add_u32 {d0}, {d0}, {o(j)}")
+        L.append(f"v_mad_u64_u32 {D}, {SD}, {o(j + 9)}, {K31264}, {D}")
+        L.append(f"v_mad_u64_u32 {D}, {SD}, {o(j + 8)}, {K256}, {D}")
+        L.append(f"v_and_b32_e32 {o(j)}, 0x1fffffff, {d0}")
+    # limb 8: o_8 + carry + 31264 o17 + 256 o_16; 24 bits stay, the rest (units of 2^256) is T
+    L.append(f"v_lshrrev_b64 {D}, 29, {D}")
+    L.append(f"v_add_u32 {d0}, {d0}, {o(8)}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {c0}, {K31264}, {D}")
+    L.append(f"v_mad_u32_u24 {d1}, {c1}, {K31264}, {d1}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {o(16)}, {K256}, {D}")
+    L.append(f"v_and_b32_e32 {o(8)}, 0xffffff, {d0}")
+    L.append(f"v_lshrrev_b64 {D}, 24, {D}")
+    L.append(f"v_lshlrev_b64 {C}, 13, {C}")             # (v_lshl_add_u64 shifts by 0..4 only)
+    L.append(f"v_lshl_add_u64 {C}, {C}, 0, {D}")        # T = (c >> 24) + (o17 << 13) < 2^49
+    # 2^256 == 2^32 + 977: limb 0 += 977 T, limb 1 += 8 T (+ carries), limb 2 += carry
+    L.append(f"v_mov_b32 {d1}, 0")
+    L.append(f"v_mov_b32 {d0}, {o(0)}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {c0}, {K977}, {D}")
+    L.append(f"v_mad_u32_u24 {d1}, {c1}, {K977}, {d1}")
+    L.append(f"v_and_b32_e32 {o(0)}, 0x1fffffff, {d0}")
+    L.append(f"v_lshrrev_b64 {D}, 29, {D}")
+    L.append(f"v_lshl_add_u64 {D}, {C}, 3, {D}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {o(1)}, 1, {D}")
+    L.append(f"v_and_b32_e32 {o(1)}, 0x1fffffff, {d0}")
+    L.append(f"v_alignbit_b32 {c0}, {d1}, {d0}, 29")
+    L.append(f"v_add_u32 {o(2)}, {o(2)}, {c0}")
+    return L
 
 
 def main():
@@ -53,17 +113,8 @@ def main():
            "// Column products of secp256k1_fe9.cuh as single inline-asm statements (see the generator's",
            "// docstring for why).  c[k] = column k of a*b plus the carry of column k-1 (c[k-1] >> 29).",
            "#pragma once", "#include <stdint.h>", "namespace gsv {"]
-    ins_mul = [f"a[{i}]" for i in range(9)] + [f"b[{j}]" for j in range(9)]
-    mul = product(lambda k: [(i, 9 + (k - i)) for i in range(9) if 0 <= k - i < 9], ins_mul)
-    out += emit("fe9_mul_cols", "a * b (81 v_mad_u64_u32, 16 v_lshrrev_b64)", mul, ins_mul)
-    # squaring: b holds the doubled limbs 2 a[j]; cross terms a[i] * 2a[j] (i < j) + a[k/2]^2
-    def sqr_terms(k):
-        t = [(i, 9 + (k - i)) for i in range(9) if i < k - i < 9]
-        if k % 2 == 0 and k // 2 < 9:
-            t.append((k // 2, k // 2))
-        return t
-    sqr = product(sqr_terms, ins_mul)
-    out += emit("fe9_sqr_cols", "a^2 with b = 2a limb-wise (45 v_mad_u64_u32, 16 v_lshrrev_b64)", sqr, ins_mul)
+    out += full("fe9_mul_full", "r = a * b mod p, weakly normalised (fe9_mul's contract)", MUL_TERMS)
+    out += full("fe9_sqr_full", "r = a^2 mod p with b = 2a limb-wise (fe9_sqr's contract)", SQR_TERMS)
     out.append("}  // namespace gsv")
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")
