@@ -20,7 +20,8 @@ constexpr int OPS = 64;
 #define R32(x) R8(x) R8(x) R8(x) R8(x)
 
 // MODE 0: fe9_mul chain, 1: fe9_sqr chain, 2: gej9_dbl chain, 3: 32 independent v_mad_u64_u32 (asm),
-// 4: 32 independent v_add_u32 (asm), 5: mixed-add gej9_add_ge_core chain
+// 4: 32 independent v_add_u32 (asm), 5: mixed-add gej9_add_ge_core chain, 6: v_lshrrev_b64,
+// 7: v_alignbit_b32, 8: v_and_b32 with a literal, 9: a dependent mad / 64-bit shift chain
 template <int MODE>
 __global__ __launch_bounds__(256) void k_occ(uint32_t* out, uint32_t seed) {
     extern __shared__ uint32_t lds[];
@@ -50,6 +51,28 @@ __global__ __launch_bounds__(256) void k_occ(uint32_t* out, uint32_t seed) {
                          : "+v"(a9.v[0]), "+v"(a9.v[1]), "+v"(a9.v[2]), "+v"(a9.v[3]), "+v"(a9.v[4]), "+v"(a9.v[5]),
                            "+v"(a9.v[6]), "+v"(a9.v[7])
                          : "v"(y0));
+        } else if (MODE == 6) {
+            asm volatile(R4("v_lshrrev_b64 %0, 29, %0\n\tv_lshrrev_b64 %1, 29, %1\n\tv_lshrrev_b64 %2, 29, %2\n\tv_lshrrev_b64 %3, 29, %3\n\t"
+                            "v_lshrrev_b64 %4, 29, %4\n\tv_lshrrev_b64 %5, 29, %5\n\tv_lshrrev_b64 %6, 29, %6\n\tv_lshrrev_b64 %7, 29, %7\n\t")
+                         : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7));
+        } else if (MODE == 7) {
+            asm volatile(R4("v_alignbit_b32 %0, %0, %8, 29\n\tv_alignbit_b32 %1, %1, %8, 29\n\tv_alignbit_b32 %2, %2, %8, 29\n\tv_alignbit_b32 %3, %3, %8, 29\n\t"
+                            "v_alignbit_b32 %4, %4, %8, 29\n\tv_alignbit_b32 %5, %5, %8, 29\n\tv_alignbit_b32 %6, %6, %8, 29\n\tv_alignbit_b32 %7, %7, %8, 29\n\t")
+                         : "+v"(a9.v[0]), "+v"(a9.v[1]), "+v"(a9.v[2]), "+v"(a9.v[3]), "+v"(a9.v[4]), "+v"(a9.v[5]),
+                           "+v"(a9.v[6]), "+v"(a9.v[7])
+                         : "v"(y0));
+        } else if (MODE == 8) {
+            asm volatile(R4("v_and_b32_e32 %0, 0x1fffffff, %8\n\tv_and_b32_e32 %1, 0x1fffffff, %8\n\tv_and_b32_e32 %2, 0x1fffffff, %8\n\tv_and_b32_e32 %3, 0x1fffffff, %8\n\t"
+                            "v_and_b32_e32 %4, 0x1fffffff, %8\n\tv_and_b32_e32 %5, 0x1fffffff, %8\n\tv_and_b32_e32 %6, 0x1fffffff, %8\n\tv_and_b32_e32 %7, 0x1fffffff, %8\n\t")
+                         : "+v"(a9.v[0]), "+v"(a9.v[1]), "+v"(a9.v[2]), "+v"(a9.v[3]), "+v"(a9.v[4]), "+v"(a9.v[5]),
+                           "+v"(a9.v[6]), "+v"(a9.v[7])
+                         : "v"(y0));
+        } else if (MODE == 9) {  // the mul's mix: 4 mads + 1 64-bit shift + 1 and, dependent as in a column
+            asm volatile(R4("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_mad_u64_u32 %0, vcc, %3, %2, %0\n\t"
+                            "v_mad_u64_u32 %0, vcc, %2, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %3, %0\n\t"
+                            "v_lshrrev_b64 %1, 29, %0\n\tv_mad_u64_u32 %1, vcc, %2, %3, %1\n\t"
+                            "v_mad_u64_u32 %1, vcc, %3, %2, %1\n\tv_lshrrev_b64 %0, 29, %1\n\t")
+                         : "+v"(x0), "+v"(x1) : "v"(y0), "v"(y1) : "vcc");
         } else {
             gsv::gej9 p, o; gsv::ge9 q; gsv::fe9 h, rr;
             p.x = a9; p.y = b9; p.z = a9; q.x = b9; q.y = a9;
@@ -75,6 +98,8 @@ int main() {
         {"fe9_mul chain", k_occ<0>, 1}, {"fe9_sqr chain", k_occ<1>, 1}, {"gej9_dbl chain", k_occ<2>, 1},
         {"gej9 mixed add (core)", k_occ<5>, 1},
         {"v_mad_u64_u32 x8 indep", k_occ<3>, 32}, {"v_add_u32 x8 indep", k_occ<4>, 32},
+        {"v_lshrrev_b64 x8 indep", k_occ<6>, 32}, {"v_alignbit_b32 x8 indep", k_occ<7>, 32},
+        {"v_and_b32 lit x8 indep", k_occ<8>, 32}, {"mad/lshr64 dep chain", k_occ<9>, 32},
     };
     for (auto& k : ks) CHECK(hipFuncSetAttribute((const void*)k.f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     int rounds = 16;
