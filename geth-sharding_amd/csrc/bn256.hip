@@ -184,6 +184,9 @@ static BN_NI void fp12_inv_p(fp12* pe, const fp12* pa) {
 // gfp12.go:113-127 with power = u; only called on cyclotomic-subgroup elements (the final
 // exponentiation's hard part), where a^-1 = conj(a): the NAF of u needs 23 products instead of the
 // 27 of its binary expansion, and the result is the same field element a^u.
+#ifndef BN_EXPU_INLINE_MUL
+#define BN_EXPU_INLINE_MUL 1
+#endif
 static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
     fp12 sum = *a;  // the leading digit: 1^2 * a
 #pragma unroll 1
@@ -193,7 +196,11 @@ static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
         if (pos || neg) {
             fp12 t = *a;
             if (neg) t.x = fp6_store(fp6_neg(t.x));
+#if BN_EXPU_INLINE_MUL
+            sum = fp12_mul_i(sum, t);
+#else
             sum = fp12_mul(sum, t);
+#endif
         }
     }
     *c = sum;
@@ -219,8 +226,7 @@ GSV_DI void gather3(T out[3], const T& mine, int base) {  // out[r] = lane (base
 }
 // fp12_cyclo_sqr_i split by coefficient pairs: role 0 squares (x4, x0) and yields c0', c3'; role 1
 // (x2, x3) -> c2', c5'; role 2 (x5, x1) -> c4', c1'
-static BN_NI void fp12_cyclo_sqr3(fp12* pe, const fp12* pa, int role, int base) {
-    const fp12 a = *pa;
+GSV_DI void fp12_cyclo_sqr3_i(fp12* pe, const fp12& a, int role, int base) {
     const fp2 &x0 = a.y.z, &x1 = a.y.y, &x2 = a.y.x, &x3 = a.x.z, &x4 = a.x.y, &x5 = a.x.x;
     fp2r p = fp2_reduce(role == 0 ? x4 : role == 1 ? x2 : x5);
     fp2r q = fp2_reduce(role == 0 ? x0 : role == 1 ? x3 : x1);
@@ -242,9 +248,11 @@ static BN_NI void fp12_cyclo_sqr3(fp12* pe, const fp12* pa, int role, int base) 
     pe->y.x = all[2].lo;
     pe->x.z = all[2].hi;
 }
+static BN_NI void fp12_cyclo_sqr3(fp12* pe, const fp12* pa, int role, int base) {
+    fp12_cyclo_sqr3_i(pe, *pa, role, base);
+}
 // fp12_mul_i's three F_p^6 products, one per role
-static BN_NI void fp12_mul3(fp12* pe, const fp12* pa, const fp12* pb, int role, int base) {
-    const fp12 a = *pa, b = *pb;
+GSV_DI void fp12_mul3_i(fp12* pe, const fp12& a, const fp12& b, int role, int base) {
     fp6 sa = fp6_store(fp6_add(a.x, a.y)), sb = fp6_store(fp6_add(b.x, b.y));
     fp6 l = role == 0 ? a.x : role == 1 ? a.y : sa;
     fp6 r = role == 0 ? b.x : role == 1 ? b.y : sb;
@@ -253,16 +261,31 @@ static BN_NI void fp12_mul3(fp12* pe, const fp12* pa, const fp12* pb, int role, 
     pe->x = fp6_store(fp6_sub(fp6_sub(v[2], v[0]), v[1]));
     pe->y = fp6_store(fp6_add(v[1], fp6_mul_tau(v[0])));
 }
+static BN_NI void fp12_mul3(fp12* pe, const fp12* pa, const fp12* pb, int role, int base) {
+    fp12_mul3_i(pe, *pa, *pb, role, base);
+}
 static BN_NI void fp12_exp_u3(fp12* c, const fp12* a, int role, int base) {
     fp12 sum = *a;
 #pragma unroll 1
     for (int i = 61; i >= 0; i--) {
+#if BN_EXPU_INLINE_MUL
+        fp12 s2v;
+        fp12_cyclo_sqr3_i(&s2v, sum, role, base);
+        sum = s2v;
+#else
         fp12_cyclo_sqr3(&sum, &sum, role, base);
+#endif
         bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
         if (pos || neg) {
             fp12 t = *a;
             if (neg) t.x = fp6_store(fp6_neg(t.x));
+#if BN_EXPU_INLINE_MUL
+            fp12 m;
+            fp12_mul3_i(&m, sum, t, role, base);
+            sum = m;
+#else
             fp12_mul3(&sum, &sum, &t, role, base);
+#endif
         }
     }
     *c = sum;
