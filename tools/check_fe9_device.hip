@@ -47,7 +47,8 @@ __global__ void k_recover(const uint8_t* msg, const uint8_t* sig, const uint4* g
     gsv::load32_be(r, sig);
     gsv::load32_be(s, sig + 32);
     gsv::fe qx, qy;
-    uint32_t st = gsv::recover_core(qx, qy, m, r, s, sig[64], gtab);
+    __shared__ uint32_t ltab[gsv::GSV_LTAB_WORDS];
+    uint32_t st = gsv::recover_core(qx, qy, m, r, s, sig[64], gtab, ltab + threadIdx.x);
     out[0] = st;
     for (int k = 0; k < 8; k++) { out[1 + k] = qx.v[k]; out[9 + k] = qy.v[k]; }
 }
@@ -79,10 +80,7 @@ int main() {
     CHECK(hipMemcpy(dm, msg, 32, hipMemcpyHostToDevice)); CHECK(hipMemcpy(ds, sig, 65, hipMemcpyHostToDevice));
     CHECK(gsv::launch_gtable_init(gtab, 0));
     CHECK(hipDeviceSynchronize());
-    std::vector<uint32_t> gt(gsv::GTAB_BYTES / 4);
-    CHECK(hipMemcpy(gt.data(), gtab, gsv::GTAB_BYTES, hipMemcpyDeviceToHost));
-    f = fopen("gpurun_out/fe9_gtab.bin", "wb"); fwrite(gt.data(), 4, gt.size(), f); fclose(f);
-    hipLaunchKernelGGL(k_recover, dim3(1), dim3(64), 0, 0, dm, ds, gtab, dout);
+    hipLaunchKernelGGL(k_recover, dim3(1), dim3(256), 0, 0, dm, ds, gtab, dout);
     CHECK(hipDeviceSynchronize());
     uint32_t ro[17];
     CHECK(hipMemcpy(ro, dout, sizeof(ro), hipMemcpyDeviceToHost));
