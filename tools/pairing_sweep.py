@@ -18,7 +18,7 @@ import gsv
 from gsv import _lib
 
 
-def run(ctx, n, k, f3=None, reps=2):
+def run(ctx, n, k, f3=None, reps=2, m2=None):
     if k:
         os.environ["GSV_BN_PAIRS_PER_LANE"] = str(k)
     else:
@@ -27,6 +27,10 @@ def run(ctx, n, k, f3=None, reps=2):
         os.environ["GSV_BN_FINAL3"] = str(f3)
     else:
         os.environ.pop("GSV_BN_FINAL3", None)
+    if m2 is not None:
+        os.environ["GSV_BN_MILLER2"] = str(m2)
+    else:
+        os.environ.pop("GSV_BN_MILLER2", None)
     pin = torch.empty((n, 768), dtype=torch.uint8, device="cuda")
     pexp = torch.empty((n,), dtype=torch.uint8, device="cuda")
     pver = torch.empty((n,), dtype=torch.uint8, device="cuda")
@@ -47,13 +51,21 @@ def run(ctx, n, k, f3=None, reps=2):
     return dt, ks
 
 
+CASES = ((0, None, None), (1, None, None), (2, None, None), (4, None, None), (0, 0, None), (0, 1, None),
+         (0, None, 0), (0, None, 1), (2, None, 1))
+if os.environ.get("SWEEP_CASES"):  # e.g. "4,,1;2,,1" = k,final3,miller2 (empty = auto)
+    CASES = tuple(tuple(int(x) if x else (0 if i == 0 else None) for i, x in enumerate(c.split(",")))
+                  for c in os.environ["SWEEP_CASES"].split(";"))
+
+
 def main():
     sizes = [int(a) for a in sys.argv[1:]] or [65536, 32768, 16384, 8192]
     ctx = gsv.default_context()
     for n in sizes:
-        for k, f3 in ((0, None), (1, None), (2, None), (4, None), (0, 0), (0, 1)):
-            dt, ks = run(ctx, n, k, f3)
-            print(f"checks {n:6d} k {k or 'auto':>4} final3 {'auto' if f3 is None else f3:>4}: {dt * 1e3:8.2f} ms  "
+        for k, f3, m2 in CASES:
+            dt, ks = run(ctx, n, k, f3, m2=m2)
+            print(f"checks {n:6d} k {k or 'auto':>4} final3 {'auto' if f3 is None else f3:>4} "
+                  f"miller2 {'auto' if m2 is None else m2:>4}: {dt * 1e3:8.2f} ms  "
                   f"{n / dt / 1e6:.3f} M checks/s  prepare/miller/final {ks[0]:.2f}/{ks[1]:.2f}/{ks[2]:.2f} ms",
                   flush=True)
 
