@@ -352,19 +352,30 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
     rng = np.random.default_rng(99 + rank)
     bodies = torch.from_numpy(rng.integers(0, 256, N_SHARDS * BODY, dtype=np.uint8)).to(dev)
     h_off = np.arange(N_SHARDS + 1, dtype=np.uint64) * BODY
-    roots = torch.empty((N_SHARDS, 32), dtype=torch.uint8, device=dev)
+    # consecutive batches go to `depth` streams, each with its own instance of the prepared shape
+    # (gsv_ctx_set_pipeline_depth): the latency-bound top of one batch's trie runs under the next
+    # batch's leaf level, as a notary validating a stream of collations would run them
+    depth = max(1, args.pipeline)
+    ctx.set_pipeline_depth(depth)
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
+    rootk = [torch.empty((N_SHARDS, 32), dtype=torch.uint8, device=dev) for _ in range(depth)]
+    roots = rootk[0]
     ctx.chunk_root_prepare(h_off)
+    ctx.set_pipeline_depth(1)
     csteps = max(4, args.steps)
-    for _ in range(max(1, args.warmup)):
-        ctx.chunk_root_batch_dev(bodies, h_off, roots, stream=stream, prepare=False)
-    stream.synchronize()
+    for i in range(max(depth, args.warmup)):
+        ctx.chunk_root_batch_dev(bodies, h_off, rootk[i % depth], stream=streams[i % depth], prepare=False)
+    for s_ in streams:
+        s_.synchronize()
+    assert all(torch.equal(r, roots) for r in rootk), "pipelined chunk roots differ between instances"
     # timed region without kernel-timing events (a step is ~10 short launches; an event pair
     # around each would add ~15 % to the step)
     barrier(ws)
     t1 = time.perf_counter()
-    for _ in range(csteps):
-        ctx.chunk_root_batch_dev(bodies, h_off, roots, stream=stream, prepare=False)
-    stream.synchronize()
+    for i in range(csteps):
+        ctx.chunk_root_batch_dev(bodies, h_off, rootk[i % depth], stream=streams[i % depth], prepare=False)
+    for s_ in streams:
+        s_.synchronize()
     barrier(ws)
     cdt = max_over_ranks(time.perf_counter() - t1, ws)
     # per-kernel breakdown from a separate, instrumented pass
@@ -401,6 +412,7 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
             "permutations_per_launch": bot_perms}
     out = {"collation_GBps": round(ws * N_SHARDS * BODY * csteps / cdt / 1e9, 3),
            "shards": N_SHARDS * ws, "body_bytes": BODY, "ms_per_step": round(cdt / csteps * 1e3, 3),
+           "pipeline_depth": depth,
            "permutations_per_s": round(perms_s, 1),
            "bottom_kernel_avg_ms": round(bot_ms, 4),
            "level_kernels_ms_per_step": round(lvl_ms / 2, 4), "roofline": roof}
@@ -628,21 +640,37 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     ctx.bn256_synth_checks_dev(5000 + rank, pin, pexp, stream=stream)
     p_off = np.arange(nloc + 1, dtype=np.uint64) * 768
     stream.synchronize()
+    # consecutive batches on `depth` streams with their own shape instances (as the chunk-root leg):
+    # one batch's latency-bound Miller / final-exponentiation waves share the SIMDs with the next
+    # batch's kernels
+    depth = max(1, args.pairing_pipeline)
+    ctx.set_pipeline_depth(depth)
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
+    pvk = [pver] + [torch.empty_like(pver) for _ in range(depth - 1)]
     ctx.pairing_prepare(p_off)
-    ctx.pairing_check_batch_dev(pin, p_off, pver, stream=stream, prepare=False)  # warmup
-    stream.synchronize()
+    ctx.set_pipeline_depth(1)
+    for i in range(depth):  # warmup
+        ctx.pairing_check_batch_dev(pin, p_off, pvk[i], stream=streams[i], prepare=False)
+    for s_ in streams:
+        s_.synchronize()
     # size-independent parity property at full size: every verdict equals the generator's
-    assert torch.equal(pver, pexp), "pairing verdicts differ from the constructed truth"
-    psteps = 2
-    ctx.reset_timing()
-    ctx.set_timing(True)
+    assert all(torch.equal(v, pexp) for v in pvk), "pairing verdicts differ from the constructed truth"
+    psteps = 6 if depth <= 3 else 2 * depth
     barrier(ws)
     t2 = time.perf_counter()
+    for i in range(psteps):
+        ctx.pairing_check_batch_dev(pin, p_off, pvk[i % depth], stream=streams[i % depth], prepare=False)
+    for s_ in streams:
+        s_.synchronize()
+    barrier(ws)
+    pdt = max_over_ranks(time.perf_counter() - t2, ws)
+    assert all(torch.equal(v, pexp) for v in pvk), "pairing verdicts differ from the constructed truth"
+    # per-kernel breakdown from a separate, instrumented single-stream pass
+    ctx.reset_timing()
+    ctx.set_timing(True)
     for _ in range(psteps):
         ctx.pairing_check_batch_dev(pin, p_off, pver, stream=stream, prepare=False)
     stream.synchronize()
-    barrier(ws)
-    pdt = max_over_ranks(time.perf_counter() - t2, ws)
     ctx.set_timing(False)
     k_prep, _ = ctx.kernel_time(_lib.K_BN_PREPARE)
     k_mill, _ = ctx.kernel_time(_lib.K_PAIRING)
@@ -669,6 +697,7 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
                                     "psi subgroup test, precomputed lines, multi-Miller loop; instrumented build, "
                                     "profiles/r02/opcount.json)"}
     out = {"checks_per_s": round(N_CHECKS * psteps / pdt, 1), "checks": N_CHECKS, "checks_per_rank": nloc,
+           "pipeline_depth": depth,
            "pairs_per_check": 4, "roofline": roof, "ms_per_step": round(pdt / psteps * 1e3, 3),
            "prepare_kernel_ms": round(k_prep / psteps, 3), "miller_kernel_ms": round(k_mill / psteps, 3),
            "final_exp_kernel_ms": round(k_fin / psteps, 3),
@@ -765,6 +794,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--legs", default=",".join(LEGS), help="comma list of " + ",".join(LEGS))
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="streams (shape instances) consecutive chunk-root batches are spread over")
+    ap.add_argument("--pairing-pipeline", type=int, default=2,
+                    help="streams (shape instances) consecutive pairing batches are spread over")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rank plumbing only (no GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -1076,6 +1076,9 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         if (e != hipSuccess) return e;
     }
     if (nchecks) {
+        // the tail: Miller loop + final exponentiation at ~one wave per SIMD (marking after the Miller
+        // loop instead, or not at all, measured the same or lower: profiles/r02/ab_pipeline.txt)
+        if (timer_begin) timer_begin(tctx, GSV_HOOK_TAIL);
         if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
         if (layout & GSV_BN_LAYOUT_MILLER2)
             hipLaunchKernelGGL(bn::k_bn_miller2, dim3((2 * nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,

@@ -910,6 +910,7 @@ static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipSt
     }
     if (top_h <= p.height) {
         if (p.height > TOP_MAX_H) return hipErrorInvalidValue;
+        if (timer_begin) timer_begin(tctx, GSV_HOOK_TAIL);
         TopLevels tl{};
         tl.h0 = top_h;
         tl.h1 = p.height;

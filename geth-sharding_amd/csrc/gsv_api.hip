@@ -7,7 +7,10 @@
 // copies of offset tables, pairing lane tables, its workspace) lives in a PREPARED SHAPE built by the
 // matching gsv_*_prepare call (which may allocate and synchronize) and cached per context, keyed by
 // exactly those host-side arguments.  A *_dev call whose shape was not prepared returns
-// GSV_E_NOT_PREPARED without touching the device.
+// GSV_E_NOT_PREPARED without touching the device.  With a pipeline depth D > 1
+// (gsv_ctx_set_pipeline_depth) a shape holds D instances of its device memory, so calls of the same
+// shape on up to D streams run concurrently (a notary validating consecutive collation batches keeps
+// the latency-bound top of one batch's trie under the next batch's leaf level).
 #include <rccl/rccl.h>
 #include <hip/hip_runtime.h>
 
@@ -67,10 +70,18 @@ struct Shape {
     uint64_t kind = 0;
     std::vector<uint64_t> key;
     uint8_t* mem = nullptr;
-    size_t bytes = 0;
+    size_t bytes = 0;   // one instance
+    int ninst = 1;      // instances of the device memory (pipeline depth at prepare time)
+    int cur = 0;        // instance of the run in progress (set by shape_run under the context's smu)
+    int rr = 0;         // next instance to recycle when every instance was last used on another stream
     bool owned = true;  // false: carved from the host-path arena
-    hipEvent_t ev = nullptr;     // recorded after the last (non-captured) use
-    hipStream_t last = nullptr;  // stream of that use
+    std::vector<hipEvent_t> ev;     // per instance: recorded after its last (non-captured) use
+    std::vector<hipStream_t> last;  // per instance: stream of that use
+    // pipelined instances: per instance, recorded where its last run's bulk kernels ended
+    // (GSV_HOOK_TAIL); the next run on another instance starts its bulk kernels after that point
+    std::vector<hipEvent_t> bulk_ev;
+    std::vector<char> bulk_rec;
+    int prev = -1;  // instance of the previous run
     std::vector<std::pair<size_t, std::vector<uint8_t>>> uploads;  // host tables, copied at prepare
     ChunkLaunch chunk;  // SK_CHUNK, SK_NOTARY, SK_POC
     // SK_PAIRING
@@ -97,7 +108,10 @@ struct Shape {
     Shape(const Shape&) = delete;
     Shape& operator=(const Shape&) = delete;
     ~Shape() {
-        if (ev) hipEventDestroy(ev);
+        for (hipEvent_t e : ev)
+            if (e) hipEventDestroy(e);
+        for (hipEvent_t e : bulk_ev)
+            if (e) hipEventDestroy(e);
         if (owned && mem) hipFree(mem);
     }
     template <typename T>
@@ -107,7 +121,7 @@ struct Shape {
         uploads.emplace_back(off, std::vector<uint8_t>(b, b + count * sizeof(T)));
     }
     template <typename T>
-    T* at(size_t off) const { return (T*)(mem + off); }
+    T* at(size_t off) const { return (T*)(mem + (size_t)cur * bytes + off); }
 };
 
 constexpr size_t kMaxShapes = 32;
@@ -134,6 +148,7 @@ struct gsv_ctx {
     std::vector<hipEvent_t> open_ev;  // timer events opened by launch hooks
     hipStream_t cur_stream = nullptr;  // stream of the shape run in progress (launch hooks)
     bool cur_capture = false;          // that run is being captured into a graph: no timer events
+    Shape* cur_shape = nullptr;        // the shape of that run (GSV_HOOK_TAIL marks)
     // trie plans per body length, prepared shapes (most recently used first)
     gsv::PlanCache plans;
     std::list<std::unique_ptr<Shape>> shapes;
@@ -142,6 +157,7 @@ struct gsv_ctx {
     // RCCL communicator of the shard partition (gsv_comm_init), nullptr = single rank
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    int pipeline_depth = 1;  // instances per prepared shape (gsv_ctx_set_pipeline_depth)
 };
 
 namespace {
@@ -212,6 +228,14 @@ void drain_timing(gsv_ctx* c) {
 // timer hooks for multi-launch paths (chunk-root levels, pairing stages)
 void hook_begin(void* p, int kid) {
     gsv_ctx* c = (gsv_ctx*)p;
+    if (kid == gsv::GSV_HOOK_TAIL) {  // the run's bulk kernels are enqueued: mark the point for the next run
+        Shape* s = c->cur_shape;
+        if (s && !c->cur_capture && !s->bulk_ev.empty()) {
+            hipEventRecord(s->bulk_ev[s->cur], c->cur_stream);
+            s->bulk_rec[s->cur] = 1;
+        }
+        return;
+    }
     if (!c->timing || c->cur_capture) return;
     std::lock_guard<std::mutex> g(c->tmu);
     hipEvent_t a = take_event(c);
@@ -258,21 +282,39 @@ struct Carve {
 };
 
 // ------------------------------------------------------------------ prepared shapes
-// allocates (or, for a host-path shape, carves) the shape's memory and uploads its host tables
-int shape_materialize(Shape& s, size_t bytes, uint8_t* carve = nullptr) {
+// allocates `ninst` instances (or, for a host-path shape, carves one) of the shape's memory and
+// uploads its host tables into each
+int shape_materialize(Shape& s, size_t bytes, uint8_t* carve = nullptr, int ninst = 1) {
+    bytes = al(bytes ? bytes : 1);
     s.bytes = bytes;
+    s.ninst = carve ? 1 : std::max(ninst, 1);
     if (carve) {
         s.mem = carve;
         s.owned = false;
-    } else if (hipMalloc(&s.mem, bytes ? bytes : 256) != hipSuccess) {
+    } else if (hipMalloc(&s.mem, bytes * s.ninst) != hipSuccess) {
         s.mem = nullptr;
         return GSV_E_NOMEM;
     }
-    for (auto& u : s.uploads) HIPCHK(hipMemcpy(s.mem + u.first, u.second.data(), u.second.size(), hipMemcpyHostToDevice));
+    for (int k = 0; k < s.ninst; k++)
+        for (auto& u : s.uploads)
+            HIPCHK(hipMemcpy(s.mem + (size_t)k * bytes + u.first, u.second.data(), u.second.size(), hipMemcpyHostToDevice));
     s.uploads.clear();
     s.uploads.shrink_to_fit();
-    if (s.owned) HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+    s.ev.assign(s.ninst, nullptr);
+    s.last.assign(s.ninst, nullptr);
+    if (s.owned)
+        for (auto& e : s.ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    s.bulk_ev.assign(s.ninst > 1 ? s.ninst : 0, nullptr);
+    s.bulk_rec.assign(s.bulk_ev.size(), 0);
+    for (auto& e : s.bulk_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return GSV_SUCCESS;
+}
+
+size_t shape_total_bytes(const Shape& s) { return s.bytes * (size_t)s.ninst; }
+
+void shape_drain(Shape& s) {
+    for (hipEvent_t e : s.ev)
+        if (e) hipEventSynchronize(e);
 }
 
 Shape* shape_find(gsv_ctx* c, uint64_t kind, const std::vector<uint64_t>& key) {
@@ -289,14 +331,39 @@ Shape* shape_find(gsv_ctx* c, uint64_t kind, const std::vector<uint64_t>& key) {
 // inserts a materialized shape; drops least-recently-used shapes beyond the bounds (after their
 // queued work has drained — a graph captured from a dropped shape must not be replayed)
 void shape_insert(gsv_ctx* c, std::unique_ptr<Shape> s) {
-    c->shape_bytes += s->bytes;
+    c->shape_bytes += shape_total_bytes(*s);
     c->shapes.push_front(std::move(s));
     while (c->shapes.size() > 1 && (c->shapes.size() > kMaxShapes || c->shape_bytes > kMaxShapeBytes)) {
         Shape* v = c->shapes.back().get();
-        if (v->ev) hipEventSynchronize(v->ev);
-        c->shape_bytes -= v->bytes;
+        shape_drain(*v);
+        c->shape_bytes -= shape_total_bytes(*v);
         c->shapes.pop_back();
     }
+}
+
+// drops the cached shape `s` (after its queued work has drained)
+void shape_erase(gsv_ctx* c, Shape* s) {
+    for (auto it = c->shapes.begin(); it != c->shapes.end(); ++it)
+        if (it->get() == s) {
+            shape_drain(*s);
+            c->shape_bytes -= shape_total_bytes(*s);
+            c->shapes.erase(it);
+            return;
+        }
+}
+
+// The instance a run on `st` uses: the one last used on `st` (the stream orders it), else one never
+// used, else the next in turn, ordered after its previous use.  Inside a capture: the instance last
+// used on `st`, else instance 0 (the caller orders graph replays against other uses of the shape).
+int shape_pick(Shape& s, hipStream_t st, bool cap) {
+    for (int k = 0; k < s.ninst; k++)
+        if (s.last[k] == st) return k;
+    if (cap) return 0;
+    for (int k = 0; k < s.ninst; k++)
+        if (!s.last[k]) return k;
+    int k = s.rr;
+    s.rr = (s.rr + 1) % s.ninst;
+    return k;
 }
 
 // Runs a shape's launches on `st`.  Users of one shape on different streams are ordered on the GPU
@@ -305,14 +372,26 @@ void shape_insert(gsv_ctx* c, std::unique_ptr<Shape> s) {
 template <typename F>
 int shape_run(gsv_ctx* c, Shape& s, hipStream_t st, F&& body) {
     bool cap = capturing(st);
-    if (!cap && s.ev && s.last && s.last != st) HIPCHK(hipStreamWaitEvent(st, s.ev, 0));
+    int k = shape_pick(s, st, cap);
+    s.cur = k;
+    if (!cap && s.ev[k] && s.last[k] && s.last[k] != st) HIPCHK(hipStreamWaitEvent(st, s.ev[k], 0));
+    if (!cap && !s.bulk_ev.empty()) {
+        // staggered pipeline: this run's bulk kernels follow the previous run's (on the other
+        // instance), so they overlap that run's latency-bound tail rather than its bulk kernels
+        if (s.prev >= 0 && s.prev != k && s.bulk_rec[s.prev]) HIPCHK(hipStreamWaitEvent(st, s.bulk_ev[s.prev], 0));
+        s.bulk_rec[k] = 0;
+        s.prev = k;
+    }
     c->cur_stream = st;
     c->cur_capture = cap;
+    c->cur_shape = &s;
     int rc = body();
+    c->cur_shape = nullptr;
+    s.cur = 0;
     if (rc) return rc;
-    if (!cap && s.ev) {
-        HIPCHK(hipEventRecord(s.ev, st));
-        s.last = st;
+    if (!cap && s.ev[k]) {
+        HIPCHK(hipEventRecord(s.ev[k], st));
+        s.last[k] = st;
     }
     return GSV_SUCCESS;
 }
@@ -470,6 +549,13 @@ void gsv_ctx_destroy(gsv_ctx* c) {
 int gsv_ctx_set_timing(gsv_ctx* c, int enable) {
     if (!c) return GSV_E_INVALID_ARG;
     c->timing = enable ? 1 : 0;
+    return GSV_SUCCESS;
+}
+
+int gsv_ctx_set_pipeline_depth(gsv_ctx* c, int depth) {
+    if (!c || depth < 1 || depth > GSV_MAX_PIPELINE_DEPTH) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->smu);
+    c->pipeline_depth = depth;
     return GSV_SUCCESS;
 }
 
@@ -1007,12 +1093,16 @@ int header_shape(gsv_ctx*, Shape& s, size_t n, Layout& L) {
 template <typename B>
 int shape_get(gsv_ctx* c, uint64_t kind, std::vector<uint64_t>&& key, B&& build, Shape** out) {
     Shape* s = shape_find(c, kind, key);
+    if (s && s->ninst < c->pipeline_depth) {  // prepared before the depth was raised: rebuild
+        shape_erase(c, s);
+        s = nullptr;
+    }
     if (!s) {
         auto ns = std::make_unique<Shape>();
         Layout L;
         int rc = build(*ns, L);
         if (rc) return rc;
-        rc = shape_materialize(*ns, L.n);
+        rc = shape_materialize(*ns, L.n, nullptr, c->pipeline_depth);
         if (rc) return rc;
         ns->kind = kind;
         ns->key = std::move(key);

@@ -23,6 +23,11 @@ hipError_t launch_synth_sign(uint64_t seed, uint32_t n, const uint4* gtab, uint8
 hipError_t launch_keccak256(const uint8_t* data, const uint64_t* off, uint32_t n, uint8_t* out32,
                             hipStream_t st);
 
+// Launchers call timer_begin(tctx, GSV_HOOK_TAIL) (no launch follows it directly) where the call's
+// bulk kernels end and its latency-bound tail begins (trie top, Miller loop + final exponentiation):
+// with pipelined shape instances the next call's bulk kernels start there (gsv_api.hip shape_run).
+constexpr int GSV_HOOK_TAIL = -1;
+
 // chunk_root.hip
 struct TriePlan;  // host-built, device-resident trie shape for one body length N
 size_t chunk_root_scratch_bytes(const TriePlan* plan, uint32_t nbodies);

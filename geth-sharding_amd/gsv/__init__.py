@@ -81,6 +81,11 @@ class Context:
         check(_lib.load().gsv_ctx_kernel_time(self._h, kid, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def set_pipeline_depth(self, depth: int):
+        """Instances per prepared shape from now on (gsv_ctx_set_pipeline_depth): *_dev calls of one
+        shape on up to `depth` streams run concurrently."""
+        check(_lib.load().gsv_ctx_set_pipeline_depth(self._h, int(depth)))
+
     def reset_timing(self):
         check(_lib.load().gsv_ctx_reset_timing(self._h))
 

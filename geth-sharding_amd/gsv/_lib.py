@@ -99,6 +99,7 @@ SIGNATURES = [
     ("gsv_collation_header_verify_batch_dev", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp,
                                                              _vp]),
     ("gsv_ctx_prepared_shapes", ctypes.c_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
+    ("gsv_ctx_set_pipeline_depth", ctypes.c_int, [_vp, ctypes.c_int]),
     ("gsv_ecrecover_precompile_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("gsv_ecrecover_precompile_batch_dev", ctypes.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
     ("gsv_chunk_root_prepare", ctypes.c_int, [_vp, _vp, _sz]),

@@ -125,6 +125,14 @@ int gsv_ctx_kernel_time(gsv_ctx *ctx, int kid, double *total_ms, long *launches)
 int gsv_ctx_reset_timing(gsv_ctx *ctx);
 /* prepared *_dev shapes currently cached and their device bytes */
 int gsv_ctx_prepared_shapes(gsv_ctx *ctx, size_t *count, size_t *device_bytes);
+/* Pipeline depth D (1..GSV_MAX_PIPELINE_DEPTH, default 1) of the shapes prepared from now on: each
+ * holds D instances of its device memory (tables and workspace), so *_dev calls of ONE shape on up to
+ * D different streams run concurrently instead of being ordered after each other (a stream keeps
+ * the instance it last used).  A shape prepared at a lower depth is rebuilt by its next prepare.
+ * Use: validating consecutive batches of equal shape on two streams overlaps one batch's
+ * latency-bound tail (trie top, final exponentiation) with the next batch's bulk kernels. */
+#define GSV_MAX_PIPELINE_DEPTH 8
+int gsv_ctx_set_pipeline_depth(gsv_ctx *ctx, int depth);
 
 /* ---- Keccak-256 (A10) ----
  * Message i is data[off[i] .. off[i+1]); out32[32*i .. +32) = Keccak256(message i). */

@@ -247,3 +247,52 @@ def test_dev_calls_capture_into_a_hip_graph(ctx, oracle):
     assert bytes(troots[0].cpu().numpy()) == oracle.derive_sha(items[:40])
     assert bytes(troots[1].cpu().numpy()) == oracle.derive_sha([])
     assert bytes(troots[2].cpu().numpy()) == oracle.derive_sha(items[40:90])
+
+
+def test_pipeline_depth_instances_run_concurrently_and_agree(ctx, oracle):
+    """gsv_ctx_set_pipeline_depth: a shape prepared at depth 2 holds two instances, consecutive calls on
+    two streams use one each (no ordering between them), and every call's results are the
+    single-stream ones; a stream keeps its instance, and depth 1 again leaves later shapes single."""
+    import torch
+    from gsv import GsvError, _lib
+    dev = torch.device("cuda", ctx.device)
+    rng = np.random.default_rng(515)
+    lens = [65536, 65536, 300, 0, 70000, 65536]  # a shape no other test prepares
+    h_off = np.zeros(len(lens) + 1, np.uint64)
+    h_off[1:] = np.cumsum(lens)
+    body_np = rng.integers(0, 256, int(h_off[-1]), dtype=np.uint8)
+    bodies = torch.from_numpy(body_np).to(dev)
+    want = ctx.chunk_root_batch([body_np[int(h_off[i]):int(h_off[i + 1])].tobytes() for i in range(len(lens))])
+    for i in (2, 3):  # spot-check against the oracle (full-size bodies are covered elsewhere)
+        assert bytes(want[i]) == oracle.derive_sha_bytes(body_np[int(h_off[i]):int(h_off[i + 1])].tobytes())
+    nchk = 96
+    pin = torch.empty((nchk, 768), dtype=torch.uint8, device=dev)
+    pexp = torch.empty((nchk,), dtype=torch.uint8, device=dev)
+    ctx.bn256_synth_checks_dev(61, pin, pexp)
+    p_off = np.arange(nchk + 1, dtype=np.uint64) * 768
+    p_off[-1] -= 7  # ragged last check -> BAD_INPUT
+    n0, b0 = ctx.prepared_shapes()
+    ctx.set_pipeline_depth(2)
+    ctx.chunk_root_prepare(h_off)
+    ctx.pairing_prepare(p_off)
+    ctx.set_pipeline_depth(1)
+    torch.cuda.synchronize()  # the synthetic checks were written on the context's stream
+    n1, b1 = ctx.prepared_shapes()
+    assert n1 == n0 + 2 and b1 > b0
+    with pytest.raises(GsvError) as e:
+        ctx.set_pipeline_depth(0)
+    assert e.value.code == _lib.E_INVALID_ARG
+    ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    roots = [torch.zeros((len(lens), 32), dtype=torch.uint8, device=dev) for _ in range(4)]
+    pv = [torch.full((nchk,), 7, dtype=torch.uint8, device=dev) for _ in range(4)]
+    for i in range(4):  # calls 0, 2 on stream 0 and 1, 3 on stream 1: the two instances in flight together
+        ctx.chunk_root_batch_dev(bodies, h_off, roots[i], stream=ss[i % 2], prepare=False)
+        ctx.pairing_check_batch_dev(pin, p_off, pv[i], stream=ss[i % 2], prepare=False)
+    for s in ss:
+        s.synchronize()
+    for i in range(4):
+        assert np.array_equal(roots[i].cpu().numpy(), want)
+        assert torch.equal(pv[i][:-1], pexp[:-1]) and int(pv[i][-1]) == _lib.PAIRING_BAD_INPUT
+    # re-preparing at depth 1 keeps the two-instance shapes (a higher depth is never dropped)
+    ctx.chunk_root_prepare(h_off)
+    assert ctx.prepared_shapes() == (n1, b1)
