@@ -108,6 +108,27 @@ def test_normalize(lib):
         lib.h_norm_full(f)
         assert val(f) == val(l) % P
         assert all(x <= M29 for x in f)
+        # the cheap zero test on weakly normalised values agrees with the full one
+        assert lib.h_is_zero_weak(w) == (val(l) % P == 0)
+
+
+def test_is_zero_weak_edges(lib):
+    """fe9_is_zero_weak on every weak form of 0 and p it can meet (normalize_weak outputs of
+    multiples of p, and mul/sqr outputs with limb 2 up to 2^29 + 2^24) and on near misses."""
+    rng = random.Random(15)
+    vals = [0, P, 2 * P, 3 * P, 7 * P, 1, P - 1, P + 1, 2**256, 2**29, 2**58]
+    for x in vals:
+        l = from_int(x) if x < 2**261 else None
+        w = arr(l)
+        lib.h_norm_weak(w)
+        assert lib.h_is_zero_weak(w) == (x % P == 0)
+    for _ in range(2000):  # product outputs: limb 2 in [0, 2^29 + 2^24), others canonical
+        l = [rng.randrange(2**29) for _ in range(9)]
+        l[2] = rng.randrange(2**29 + 2**24)
+        l[8] = rng.randrange(2**24)
+        if rng.random() < 0.3:
+            l = list(from_int(P if rng.random() < 0.5 else 0))
+        assert lib.h_is_zero_weak(arr(l)) == (val(l) % P == 0)
 
 
 def test_words_roundtrip(lib):
