@@ -58,9 +58,41 @@ if os.environ.get("SWEEP_CASES"):  # e.g. "4,,1;2,,1" = k,final3,miller2 (empty 
                   for c in os.environ["SWEEP_CASES"].split(";"))
 
 
+def run_pipelined(ctx, n, depth, steps=12):
+    """n checks per batch, consecutive batches over `depth` streams (gsv_ctx_set_pipeline_depth)"""
+    for v in ("GSV_BN_PAIRS_PER_LANE", "GSV_BN_FINAL3", "GSV_BN_MILLER2"):
+        os.environ.pop(v, None)
+    pin = torch.empty((n, 768), dtype=torch.uint8, device="cuda")
+    pexp = torch.empty((n,), dtype=torch.uint8, device="cuda")
+    ctx.bn256_synth_checks_dev(5000, pin, pexp)
+    torch.cuda.synchronize()
+    off = np.arange(n + 1, dtype=np.uint64) * 768
+    ctx.set_pipeline_depth(depth)
+    ctx.pairing_prepare(off)
+    ctx.set_pipeline_depth(1)
+    ss = [torch.cuda.Stream() for _ in range(depth)]
+    pv = [torch.empty((n,), dtype=torch.uint8, device="cuda") for _ in range(depth)]
+    for i in range(depth):
+        ctx.pairing_check_batch_dev(pin, off, pv[i], stream=ss[i], prepare=False)
+    torch.cuda.synchronize()
+    assert all(torch.equal(v, pexp) for v in pv), "verdicts differ from the constructed truth"
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ctx.pairing_check_batch_dev(pin, off, pv[i % depth], stream=ss[i % depth], prepare=False)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
 def main():
     sizes = [int(a) for a in sys.argv[1:]] or [65536, 32768, 16384, 8192]
     ctx = gsv.default_context()
+    if os.environ.get("SWEEP_PIPELINE"):  # e.g. "1,2,3": pipeline depths at auto layout
+        for n in sizes:
+            for d in (int(x) for x in os.environ["SWEEP_PIPELINE"].split(",")):
+                dt = run_pipelined(ctx, n, d)
+                print(f"checks {n:6d} pipeline depth {d}: {dt * 1e3:8.2f} ms per batch  {n / dt / 1e6:.3f} M checks/s",
+                      flush=True)
+        return
     for n in sizes:
         for k, f3, m2 in CASES:
             dt, ks = run(ctx, n, k, f3, m2=m2)
