@@ -18,9 +18,9 @@
 //     (libsecp-style "global z") so all table points are affine without an inversion; the lambda
 //     half uses (beta x, y).  128 doublings + 66 mixed additions (w = 3 with the 4-entry table in
 //     LDS: 129 + 88, measured 6 % slower: 15.5 -> 14.5 ms per 2^20 recoveries).
-//   * u1*G: fixed-base comb, 16 windows of 16 bits from an 80 MiB affine table in HBM (Infinity-Cache
-//     resident, one random 80-byte entry per window, prefetched a window ahead), 16 mixed additions
-//     and no doublings (gsv_internal.h COMB_BITS).
+//   * u1*G: fixed-base comb, 13 windows of 20 bits from a 1.09 GB affine table in HBM (one random
+//     80-byte entry per window, prefetched a window ahead), 13 mixed additions and no doublings
+//     (gsv_internal.h COMB_BITS; 16-bit windows from the Infinity Cache were 1.3 % slower).
 //   * one general Jacobian add to combine, one field inversion to affine, fused Keccak-256 address.
 #include "opcount.cuh"
 #include "recover_dev.cuh"

@@ -85,14 +85,17 @@ hipError_t launch_notary_synth(uint64_t seed, uint32_t shard0, uint32_t n_shards
                                const uint4* gtab, uint8_t* d_bodies, uint8_t* d_exp_status, uint8_t* d_exp_sender,
                                hipStream_t st);
 
-// fixed-base comb for u1*G: 256 / COMB_BITS windows of 2^COMB_BITS affine entries d * 2^(COMB_BITS w) * G.
-// 16-bit windows: 16 mixed adds per u1*G, an 80 MiB table (Infinity-Cache resident, one random 80-byte
-// read per window, prefetched a window ahead); 8-bit windows: 32 adds, 640 KiB.
+// fixed-base comb for u1*G: ceil(256 / COMB_BITS) windows of 2^COMB_BITS affine entries d * 2^(COMB_BITS w) * G.
+// 20-bit windows: 13 mixed adds per u1*G over a 1.09 GB table in HBM (one random 80-byte read per
+// window, prefetched a window ahead); 16-bit: 16 adds, 80 MiB (Infinity-Cache resident), 1.3 % slower;
+// 22-bit: 12 adds, 4 GB, within 0.1 % of 20-bit (profiles/r02/ab_comb.txt).  The table is built once
+// per context (k_gtable_base + k_gtable_init).
 #ifndef GSV_COMB_BITS
-#define GSV_COMB_BITS 16
+#define GSV_COMB_BITS 20
 #endif
 constexpr int COMB_BITS = GSV_COMB_BITS;
-constexpr int COMB_WINDOWS = 256 / COMB_BITS;
+constexpr int COMB_WINDOWS = (256 + COMB_BITS - 1) / COMB_BITS;  // the top window may be partial
+static_assert(COMB_BITS >= 4 && COMB_BITS <= 26, "comb window width");
 constexpr size_t GTAB_ENTRIES = (size_t)COMB_WINDOWS << COMB_BITS;
 constexpr size_t GTAB_ENTRY_BYTES = 80;  // fe9 x[9] y[9] + 2 pad words (recover_dev.cuh gtab_load)
 constexpr size_t GTAB_BYTES = GTAB_ENTRIES * GTAB_ENTRY_BYTES;

@@ -229,10 +229,19 @@ GSV_DI void gtab_load(ge9& P, const uint4* e) {
     }
 }
 
-// window w's digit of the 256-bit scalar u (COMB_BITS divides 32)
+// window w's digit of the 256-bit scalar u: bits [COMB_BITS w, COMB_BITS (w + 1)), which may straddle
+// two limbs (bits past 255 are 0)
 GSV_DI uint32_t comb_digit(const sc& u, uint32_t w) {
-    constexpr uint32_t PER = 32 / COMB_BITS, MASK = (1u << COMB_BITS) - 1u;
-    return (sel_word(u.v, w / PER) >> ((w % PER) * COMB_BITS)) & MASK;
+    constexpr uint32_t MASK = (1u << COMB_BITS) - 1u;
+    if constexpr (32 % COMB_BITS == 0) {
+        constexpr uint32_t PER = 32 / COMB_BITS;
+        return (sel_word(u.v, w / PER) >> ((w % PER) * COMB_BITS)) & MASK;
+    } else {
+        const uint32_t x[9] = {u.v[0], u.v[1], u.v[2], u.v[3], u.v[4], u.v[5], u.v[6], u.v[7], 0u};
+        uint32_t bit = w * (uint32_t)COMB_BITS, k = bit >> 5, sh = bit & 31u;
+        uint64_t pair = ((uint64_t)sel_word(x, k + 1) << 32) | sel_word(x, k);
+        return (uint32_t)(pair >> sh) & MASK;
+    }
 }
 
 // u*G with the fixed-base comb table (COMB_WINDOWS mixed adds, no doublings)
