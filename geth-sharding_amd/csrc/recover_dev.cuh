@@ -41,7 +41,11 @@ __device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du
 constexpr int GLV_W = GSV_GLV_W;
 constexpr int GLV_NT = 1 << (GLV_W - 1);             // table entries
 constexpr int GLV_DIGITS = (130 + GLV_W - 1) / GLV_W;  // k + skew < 2^129 (the split's bound is 2^128)
-static_assert(GLV_W >= 3 && GLV_W <= 4 && GLV_DIGITS * 4 <= 192, "digits pack 4 bits (sign + 3-bit index) into 6 words");
+// digit code = sign bit above a (W - 1)-bit table index, packed in DIG_SLOT-bit slots
+constexpr int DIG_SLOT = GLV_W <= 4 ? 4 : 8;
+constexpr int DIG_PER_WORD = 32 / DIG_SLOT;
+constexpr int DIG_WORDS = (GLV_DIGITS + DIG_PER_WORD - 1) / DIG_PER_WORD;
+static_assert(GLV_W >= 3 && GLV_W <= 5, "GLV window width");
 // where the per-lane GLV table lives: 0 = LDS ([word][256 lanes] per block), 1 = a private array
 // (scratch: memory only for resident lanes, served by L1/L2), 2 = entries 0..3 in LDS and the rest
 // in the private array.  Two waves per SIMD leave LDS room for 72 words a lane: four entries.
@@ -107,8 +111,9 @@ GSV_DI void sc_split_lambda(sc& r1, sc& r2, const sc& k) {
 GSV_DI bool sc_is_high(const sc& a) { return limbs_lt(HALF_N, a.v); }
 
 // Fixed-schedule odd-digit recoding, w = GLV_W: k (odd after skew) = sum d_i 2^(w i) with
-// d_i odd in [-(2^w - 1), 2^w - 1].  Digit i packed in 4 bits: bit 3 = negative, bits 0-2 = (|d|-1)/2.
-GSV_DI void recode_glv(uint32_t dig[6], uint32_t& skew, const sc& kin) {
+// d_i odd in [-(2^w - 1), 2^w - 1].  Digit i packed in a DIG_SLOT-bit slot: bit w - 1 = negative,
+// bits 0 .. w - 2 = (|d| - 1) / 2.
+GSV_DI void recode_glv(uint32_t dig[DIG_WORDS], uint32_t& skew, const sc& kin) {
     constexpr uint32_t MASK = (2u << GLV_W) - 1u;
     constexpr int32_t OFF = 1 << GLV_W;
     uint32_t k[5] = {kin.v[0], kin.v[1], kin.v[2], kin.v[3], kin.v[4]};
@@ -122,7 +127,7 @@ GSV_DI void recode_glv(uint32_t dig[6], uint32_t& skew, const sc& kin) {
         k[i] = lo32(c);
     }
 #pragma unroll
-    for (int i = 0; i < 6; i++) dig[i] = 0;
+    for (int i = 0; i < DIG_WORDS; i++) dig[i] = 0;
 #pragma unroll
     for (int i = 0; i < GLV_DIGITS; i++) {
         int32_t d;
@@ -130,8 +135,8 @@ GSV_DI void recode_glv(uint32_t dig[6], uint32_t& skew, const sc& kin) {
         else d = (int32_t)(k[0] & MASK);
         uint32_t neg = d < 0 ? 1u : 0u;
         uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-        uint32_t code = (neg << 3) | ((mag - 1u) >> 1);
-        dig[i >> 3] |= code << ((i & 7) * 4);
+        uint32_t code = (neg << (GLV_W - 1)) | ((mag - 1u) >> 1);
+        dig[i / DIG_PER_WORD] |= code << ((i % DIG_PER_WORD) * DIG_SLOT);
         // k = (k - d) >> w
         int64_t t = (int64_t)k[0] - d;
         uint32_t kk[5];
@@ -351,7 +356,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
 #pragma unroll
         for (int i = 0; i < 8; i++) k2.v[i] = neg2 ? nk.v[i] : k2.v[i];
     }
-    uint32_t dig1[6], dig2[6], skew1, skew2;
+    uint32_t dig1[DIG_WORDS], dig2[DIG_WORDS], skew1, skew2;
     recode_glv(dig1, skew1, k1);
     recode_glv(dig2, skew2, k2);
 
@@ -442,8 +447,9 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
 #pragma unroll 1
             for (int d = 0; d < GLV_W; d++) gej9_dbl(acc, acc);
         }
-        uint32_t c1 = (sel_word(dig1, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
-        uint32_t c2 = (sel_word(dig2, (uint32_t)i >> 3) >> ((i & 7) * 4)) & 15u;
+        constexpr uint32_t CMASK = (1u << DIG_SLOT) - 1u;
+        uint32_t c1 = (sel_word(dig1, (uint32_t)i / DIG_PER_WORD) >> ((i % DIG_PER_WORD) * DIG_SLOT)) & CMASK;
+        uint32_t c2 = (sel_word(dig2, (uint32_t)i / DIG_PER_WORD) >> ((i % DIG_PER_WORD) * DIG_SLOT)) & CMASK;
         // one add body, two passes: digit of k1 on T, digit of k2 on lambda(T) = (beta x, y)
 #pragma unroll 1
         for (int j = 0; j < 2; j++) {
@@ -473,7 +479,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             }
             fe9 ny;
             fe9_neg<1>(ny, P.y);         // 2
-            fe9_cmov(P.y, ny, ((c >> 3) != 0) != ng);
+            fe9_cmov(P.y, ny, ((c >> (GLV_W - 1)) != 0) != ng);
             gej9_add_ge(acc, ainf, acc, P);
         }
     }
