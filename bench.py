@@ -331,9 +331,9 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
             "mac_equiv_per_recovery_actual": oc["mac_equiv"] if oc else None,
             "traffic": pmc_traffic(k), "traffic_source": "profiles/r02/pmc_all.json" if pmc_traffic(k) else None,
             "algorithmic_bytes_per_launch": N_SIGS * (32 + 65 + 65 + 20 + 1),
-            # by design: one 80-byte affine comb entry per 16-bit window of u1 (16 per recovery) from the
-            # 80 MiB Infinity-Cache-resident table
-            "comb_table_bytes_per_launch": N_SIGS * 16 * 80,
+            # by design: one 80-byte affine comb entry per 20-bit window of u1 (13 per recovery) from the
+            # 1.09 GB table in HBM (gsv_internal.h GSV_COMB_BITS)
+            "comb_table_bytes_per_launch": N_SIGS * 13 * 80,
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"), "valu_issue_peak": VALU_ISSUE_PEAK,
             "int_lane_ops": int_lane_ops(k, k.get("avg_ms")),
             "kernel": "k_ecrecover", "kernel_avg_ms": round(k_avg_ms, 4),
