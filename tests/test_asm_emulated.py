@@ -91,6 +91,10 @@ class Machine:
                 res = self.r32(a[1]) + self.r32(a[2])
                 assert res <= M32, f"32-bit overflow in {ln}"
                 self.w32(a[0], res)
+            elif op == "v_add3_u32":
+                res = self.r32(a[1]) + self.r32(a[2]) + self.r32(a[3])
+                assert res <= M32, f"32-bit overflow in {ln}"
+                self.w32(a[0], res)
             elif op == "v_mad_u32_u24":
                 x, y = self.r32(a[1]), self.r32(a[2])
                 assert x < 1 << 24 and y < 1 << 24, f"u24 operand out of range in {ln}"
@@ -136,9 +140,11 @@ def fe9_case(rng, ma, mb, extreme):
     return a, b
 
 
-def run_fe9(lines, a, b):
+def run_fe9(lines, a, b, c=None):
     ops = {18 + i: a[i] for i in range(9)}
     ops.update({27 + j: b[j] for j in range(9)})
+    if c is not None:
+        ops.update({39 + j: c[j] for j in range(9)})
     ops.update({36: 31264, 37: 256, 38: 977})
     m = Machine(ops)
     m.run(lines)
@@ -168,6 +174,37 @@ def test_fe9_sqr_asm(ma):
         a2 = [x << 1 for x in a]
         assert max(a2) <= M32
         check_weak(run_fe9(lines, a, a2), limbs_val(a) ** 2)
+
+
+Q3_MAX = [(4 << 29) - 1] * 8 + [(4 << 29) - 1]  # fe9_negsum<3> addend limbs: Q_3 limbs < 2^31
+
+
+def addend_case(rng, extreme):
+    """c of fe9_mul_add / fe9_sqr_add: Q_M - x - y (- z), M <= 3: every limb in [0, 2^31)"""
+    if extreme:
+        return list(Q3_MAX)
+    return [rng.randrange(1 << 31) for _ in range(9)]
+
+
+@pytest.mark.parametrize("ma,mb", [(1.04, 1.04), (1, 3), (1.04, 4.16), (1, 7)])
+def test_fe9_mul_add_asm(ma, mb):
+    rng = random.Random(int(ma * 1000 + mb))
+    lines = gen_fe9_asm.full_lines(gen_fe9_asm.MUL_TERMS, addend=True)
+    for it in range(150):
+        a, b = fe9_case(rng, ma, mb, extreme=(it == 0))
+        c = addend_case(rng, extreme=(it < 2))
+        check_weak(run_fe9(lines, a, b, c), limbs_val(a) * limbs_val(b) + limbs_val(c))
+
+
+@pytest.mark.parametrize("ma", [1, 1.04, 2.64])
+def test_fe9_sqr_add_asm(ma):
+    rng = random.Random(int(ma * 1000) + 7)
+    lines = gen_fe9_asm.full_lines(gen_fe9_asm.SQR_TERMS, addend=True)
+    for it in range(150):
+        a, _ = fe9_case(rng, ma, 1, extreme=(it == 0))
+        a2 = [x << 1 for x in a]
+        c = addend_case(rng, extreme=(it < 2))
+        check_weak(run_fe9(lines, a, a2, c), limbs_val(a) ** 2 + limbs_val(c))
 
 
 # --------------------------------------------------------------------------- BN254 REDC

@@ -19,14 +19,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "geth-sharding_amd", "csrc", "fe9_asm.cuh")
 
 
-def full(name, doc, terms_of_column):
-    L = full_lines(terms_of_column)
+def full(name, doc, terms_of_column, addend=False):
+    L = full_lines(terms_of_column, addend)
     outs = ", ".join([f'"=&v"(r[{i}])' for i in range(9)] + [f'"=&v"(hi[{i}])' for i in range(8)] + ['"=&s"(sd)'])
     ins = ", ".join([f'"v"(a[{i}])' for i in range(9)] + [f'"v"(b[{j}])' for j in range(9)] +
-                    ['"s"(k31264)', '"s"(k256)', '"s"(k977)'])
+                    ['"s"(k31264)', '"s"(k256)', '"s"(k977)'] +
+                    ([f'"v"(c[{j}])' for j in range(9)] if addend else []))
     body = "\\n\\t".join(L)
     return [f"// {doc}",
-            f"__device__ __forceinline__ void {name}(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]) {{",
+            f"__device__ __forceinline__ void {name}(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]"
+            + (", const uint32_t c[9]" if addend else "") + ") {",
             "    uint32_t hi[8];",
             "    uint64_t sd;",
             "    uint32_t k31264 = 31264u, k256 = 256u, k977 = 977u;",
@@ -48,11 +50,14 @@ def SQR_TERMS(k):
     return t
 
 
-def full_lines(terms_of_column):
+def full_lines(terms_of_column, addend=False):
     """Product + reduction (secp256k1_fe9.cuh fe9_reduce restated) in one statement.  Operands:
     %0..%8 r (o_0..o_8 in place), %9..%16 o_9..o_16, %17 sd, %18..%26 a, %27..%35 b,
-    %36 31264, %37 256, %38 977 (SGPRs).  Fixed pairs: C = v[2:3] (columns, then o17, then T),
-    D = v[4:5] (the reduction's running value)."""
+    %36 31264, %37 256, %38 977 (SGPRs), with `addend` %39..%47 the limbs of c (each < 2^31),
+    added to o_0..o_8 as the reduction reads them (r = a b + c; the 32-bit add that takes o_j becomes
+    a three-operand add, no further instruction).  Fixed pairs: C = v[2:3] (columns, then o17, then
+    T), D = v[4:5] (the reduction's running value)."""
+    cj = lambda j: f"%{39 + j}"
     C, c0, c1 = "v[2:3]", "v2", "v3"
     D, d0, d1 = "v[4:5]", "v4", "v5"
     o = lambda k: f"%{k}" if k < 9 else f"%{k}"
@@ -74,18 +79,27 @@ def full_lines(terms_of_column):
     L.append(f"v_lshrrev_b64 {C}, 29, {C}")               # o17 < 2^35
     # limbs 0..7: c = o_j + carry + 31264 o_{j+9} + 256 o_{j+8}
     L.append(f"v_mov_b32 {d1}, 0")
-    L.append(f"v_mov_b32 {d0}, {o(0)}")
+    if addend:
+        L.append(f"v_add_u32 {d0}, {o(0)}, {cj(0)}")       # o_0 + c_0 < 2^29 + 2^31
+    else:
+        L.append(f"v_mov_b32 {d0}, {o(0)}")
     L.append(f"v_mad_u64_u32 {D}, {SD}, {o(9)}, {K31264}, {D}")
     L.append(f"v_and_b32_e32 {o(0)}, 0x1fffffff, {d0}")
     for j in range(1, 8):
-        L.append(f"v_lshrrev_b64 {D}, 29, {D}")           # carry < 2^16: the high word is 0
-        L.append(f"v_add_u32 {d0}, {d0}, {o(j)}")
+        L.append(f"v_lshrrev_b64 {D}, 29, {D}")           # carry < 2^17: the high word is 0
+        if addend:
+            L.append(f"v_add3_u32 {d0}, {d0}, {o(j)}, {cj(j)}")
+        else:
+            L.append(f"v_add_u32 {d0}, {d0}, {o(j)}")
         L.append(f"v_mad_u64_u32 {D}, {SD}, {o(j + 9)}, {K31264}, {D}")
         L.append(f"v_mad_u64_u32 {D}, {SD}, {o(j + 8)}, {K256}, {D}")
         L.append(f"v_and_b32_e32 {o(j)}, 0x1fffffff, {d0}")
     # limb 8: o_8 + carry + 31264 o17 + 256 o_16; 24 bits stay, the rest (units of 2^256) is T
     L.append(f"v_lshrrev_b64 {D}, 29, {D}")
-    L.append(f"v_add_u32 {d0}, {d0}, {o(8)}")
+    if addend:
+        L.append(f"v_add3_u32 {d0}, {d0}, {o(8)}, {cj(8)}")
+    else:
+        L.append(f"v_add_u32 {d0}, {d0}, {o(8)}")
     L.append(f"v_mad_u64_u32 {D}, {SD}, {c0}, {K31264}, {D}")
     L.append(f"v_mad_u32_u24 {d1}, {c1}, {K31264}, {d1}")
     L.append(f"v_mad_u64_u32 {D}, {SD}, {o(16)}, {K256}, {D}")
@@ -115,6 +129,9 @@ def main():
            "#pragma once", "#include <stdint.h>", "namespace gsv {"]
     out += full("fe9_mul_full", "r = a * b mod p, weakly normalised (fe9_mul's contract)", MUL_TERMS)
     out += full("fe9_sqr_full", "r = a^2 mod p with b = 2a limb-wise (fe9_sqr's contract)", SQR_TERMS)
+    out += full("fe9_mul_add_full", "r = a * b + c mod p, c limbs < 2^31 (fe9_mul_add's contract)", MUL_TERMS, True)
+    out += full("fe9_sqr_add_full", "r = a^2 + c mod p with b = 2a limb-wise, c limbs < 2^31 (fe9_sqr_add's contract)",
+                SQR_TERMS, True)
     out.append("}  // namespace gsv")
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")
