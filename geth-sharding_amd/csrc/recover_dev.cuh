@@ -58,6 +58,10 @@ static_assert(GLV_LNT <= 4 && GLV_LNT <= GLV_NT, "LDS holds at most four entries
 // recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS].
 constexpr int GSV_LTAB_STRIDE = 256;
 constexpr int GSV_LTAB_WORDS = 18 * GLV_LNT * GSV_LTAB_STRIDE;
+// 1: the two adds of a digit position (k1 on T, k2 on lambda T) as straight-line code (A/B)
+#ifndef GSV_GLV_UNROLL_J
+#define GSV_GLV_UNROLL_J 0
+#endif
 // waves per SIMD the recovery kernels are compiled for (register budget 512 / waves)
 #ifndef GSV_ECR_WAVES
 #define GSV_ECR_WAVES 2
@@ -451,7 +455,11 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         uint32_t c1 = (sel_word(dig1, (uint32_t)i / DIG_PER_WORD) >> ((i % DIG_PER_WORD) * DIG_SLOT)) & CMASK;
         uint32_t c2 = (sel_word(dig2, (uint32_t)i / DIG_PER_WORD) >> ((i % DIG_PER_WORD) * DIG_SLOT)) & CMASK;
         // one add body, two passes: digit of k1 on T, digit of k2 on lambda(T) = (beta x, y)
+#if GSV_GLV_UNROLL_J
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
         for (int j = 0; j < 2; j++) {
             uint32_t c = j ? c2 : c1;
             bool ng = j ? neg2 : neg1;
