@@ -58,6 +58,11 @@ static_assert(GLV_LNT <= 4 && GLV_LNT <= GLV_NT, "LDS holds at most four entries
 // recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS].
 constexpr int GSV_LTAB_STRIDE = 256;
 constexpr int GSV_LTAB_WORDS = 18 * GLV_LNT * GSV_LTAB_STRIDE;
+// 1: the lambda half's x coordinates (beta x_e) precomputed per entry in a private array instead of
+// one product per lambda add (+0.3 %, profiles/r02/ab_betatab.txt)
+#ifndef GSV_GLV_BETA_TAB
+#define GSV_GLV_BETA_TAB 1
+#endif
 // 1: the two adds of a digit position (k1 on T, k2 on lambda T) as straight-line code (A/B)
 #ifndef GSV_GLV_UNROLL_J
 #define GSV_GLV_UNROLL_J 0
@@ -436,6 +441,22 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         }
         fe9_mul(zfac, D.z, P.z);  // 2*2 -> 1
     }
+#if GSV_GLV_BETA_TAB
+    uint32_t ptabB[9 * GLV_NT];  // beta x_e
+    {
+        fe9 beta;
+        fe9_from_const(beta, BETA);
+#pragma unroll
+        for (int e = 0; e < GLV_NT; e++) {
+            fe9 ex, bx;
+#pragma unroll
+            for (int k = 0; k < 9; k++) ex.v[k] = GLV_X(e, k);
+            fe9_mul(bx, ex, beta);
+#pragma unroll
+            for (int k = 0; k < 9; k++) ptabB[e * 9 + k] = bx.v[k];
+        }
+    }
+#endif
 
     gej9 acc;
     bool ainf = true;
@@ -481,9 +502,14 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
                 }
             }
             if (j != 0) {  // wave-uniform
+#if GSV_GLV_BETA_TAB
+#pragma unroll
+                for (int k = 0; k < 9; k++) P.x.v[k] = ptabB[ei * 9u + k];
+#else
                 fe9 beta;
                 fe9_from_const(beta, BETA);
                 fe9_mul(P.x, P.x, beta);
+#endif
             }
             fe9 ny;
             fe9_neg<1>(ny, P.y);         // 2
