@@ -529,9 +529,14 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             P.y.v[k] = GLV_Y(0, k);
         }
         if (j != 0) {
+#if GSV_GLV_BETA_TAB
+#pragma unroll
+            for (int k = 0; k < 9; k++) P.x.v[k] = ptabB[k];
+#else
             fe9 beta;
             fe9_from_const(beta, BETA);
             fe9_mul(P.x, P.x, beta);
+#endif
         }
         fe9 ny;
         fe9_neg<1>(ny, P.y);
