@@ -59,9 +59,11 @@ static_assert(GLV_LNT <= 4 && GLV_LNT <= GLV_NT, "LDS holds at most four entries
 constexpr int GSV_LTAB_STRIDE = 256;
 constexpr int GSV_LTAB_WORDS = 18 * GLV_LNT * GSV_LTAB_STRIDE;
 // 1: the lambda half's x coordinates (beta x_e) precomputed per entry in a private array instead of
-// one product per lambda add (+0.3 %, profiles/r02/ab_betatab.txt)
+// one product per lambda add: +0.3 % (profiles/r02/ab_betatab.txt), but the per-lane entry index
+// scatters the private-array reads over cache lines: 4.6x the kernel's fetch bytes (1.65 -> 7.6 GB
+// per 2^20 recoveries).  Off.
 #ifndef GSV_GLV_BETA_TAB
-#define GSV_GLV_BETA_TAB 1
+#define GSV_GLV_BETA_TAB 0
 #endif
 // 1: the two adds of a digit position (k1 on T, k2 on lambda T) as straight-line code (A/B)
 #ifndef GSV_GLV_UNROLL_J
