@@ -1038,8 +1038,18 @@ __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__
                                                      const uint64_t* __restrict__ leaf_base,
                                                      const uint16_t* __restrict__ leaf_depth, uint32_t N,
                                                      uint32_t nlists, uint8_t* leafrefs, uint8_t* roots) {
-    uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= (uint64_t)N * nlists) return;
+    // leaves in permutation-count order within the workgroup (keccak_dev.cuh wg_bucket_order): a
+    // leaf is its <= 16-byte header and the value, ~(L + 16) / 136 + 1 permutations
+    uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    bool valid = t0 < (uint64_t)N * nlists;
+    uint64_t blk = 0;
+    if (valid) {
+        uint64_t it0 = leaf_base[(uint32_t)(t0 / N)] + (uint32_t)(t0 % N);
+        blk = (voff[it0 + 1] - voff[it0] + 16u) / 136u;
+    }
+    uint32_t tl = wg_bucket_order((uint32_t)(t0 - (uint64_t)blockIdx.x * 256), valid, blk);
+    if (tl == ~0u) return;
+    uint64_t t = (uint64_t)blockIdx.x * 256 + tl;
     uint32_t b = (uint32_t)(t / N), j = (uint32_t)(t % N);
     uint64_t item = leaf_base[b] + j;
     const uint8_t* v = vals + voff[item];

@@ -31,40 +31,13 @@ GSV_DI void load_block(uint64_t w[17], const uint8_t* p, uint32_t avail) {
     }
 }
 
-// A lane absorbs its message's blocks in a loop, so a wave runs as many permutations as its longest
-// message: with tx-sized messages (100-160 bytes: one or two blocks) half the lanes of a wave would
-// idle through the second permutation.  Each workgroup therefore first buckets its 256 messages by
-// full-block count (LDS counters, a prefix over the buckets) and lane t takes the t-th message of
-// that order, so a wave mostly holds messages of one block count; results go to the message's own
-// slot, so the output does not depend on the order.
-constexpr uint32_t KBUCKETS = 10;  // full blocks 0..8, 9 = lanes past n
-
+// Messages are taken in block-count order within each workgroup (keccak_dev.cuh wg_bucket_order:
+// 3.21 -> 3.58 G hashes/s on tx-sized messages, profiles/r02/ab_keccak_bucket.txt).
 __global__ __launch_bounds__(256) void k_keccak256(const uint8_t* __restrict__ data,
                                                    const uint64_t* __restrict__ off, uint32_t n,
                                                    uint8_t* __restrict__ out32) {
-    __shared__ uint32_t s_cnt[KBUCKETS], s_base[KBUCKETS], s_idx[256];
-    uint32_t t = threadIdx.x;
-    uint32_t i0 = blockIdx.x * blockDim.x + t;
-    if (t < KBUCKETS) s_cnt[t] = 0;
-    __syncthreads();
-    uint32_t key = KBUCKETS - 1;
-    if (i0 < n) {
-        uint64_t nb = (off[i0 + 1] - off[i0]) / 136u;
-        key = nb < KBUCKETS - 2 ? (uint32_t)nb : KBUCKETS - 2;
-    }
-    uint32_t pos = atomicAdd(&s_cnt[key], 1u);
-    __syncthreads();
-    if (t == 0) {
-        uint32_t acc = 0;
-        for (uint32_t b = 0; b < KBUCKETS; b++) {
-            s_base[b] = acc;
-            acc += s_cnt[b];
-        }
-    }
-    __syncthreads();
-    s_idx[s_base[key] + pos] = i0;
-    __syncthreads();
-    uint32_t i = s_idx[t];
+    uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t i = wg_bucket_order(i0, i0 < n, i0 < n ? (off[i0 + 1] - off[i0]) / 136u : 0);
     if (i >= n) return;
     const uint8_t* p = data + off[i];
     uint64_t len = off[i + 1] - off[i];

@@ -203,4 +203,33 @@ GSV_DI void keccak256_xy(uint32_t h[8], const uint32_t x[8], const uint32_t y[8]
     }
 }
 
+// Lane-to-item order for a 256-thread workgroup whose lanes each absorb a variable number of rate
+// blocks: a wave runs as many permutations as its longest message, so with tx-sized messages (one or
+// two blocks) half a wave would idle through the second one.  Every thread passes its item's block
+// count (`valid` false past the end); the items are bucketed by count (LDS counters and a prefix
+// over the buckets) and the function returns the item this thread takes in that order, or ~0u.
+// Results are written to each item's own slot, so they do not depend on the order.  All 256
+// threads of the workgroup must call it (it has barriers).
+constexpr uint32_t WG_BUCKETS = 10;  // 0..8 blocks, 9 = no item
+GSV_DI uint32_t wg_bucket_order(uint32_t item, bool valid, uint64_t blocks) {
+    __shared__ uint32_t s_cnt[WG_BUCKETS], s_base[WG_BUCKETS], s_idx[256];
+    uint32_t t = threadIdx.x;
+    if (t < WG_BUCKETS) s_cnt[t] = 0;
+    __syncthreads();
+    uint32_t key = !valid ? WG_BUCKETS - 1 : blocks < WG_BUCKETS - 2 ? (uint32_t)blocks : WG_BUCKETS - 2;
+    uint32_t pos = atomicAdd(&s_cnt[key], 1u);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < WG_BUCKETS; b++) {
+            s_base[b] = acc;
+            acc += s_cnt[b];
+        }
+    }
+    __syncthreads();
+    s_idx[s_base[key] + pos] = valid ? item : ~0u;
+    __syncthreads();
+    return s_idx[t];
+}
+
 }  // namespace gsv
