@@ -13,6 +13,7 @@ enum OpKind : int {
     OPC_BN_MUL = 4,  // BN254 F_p Montgomery product
     OPC_MODINV = 5,  // safegcd inversion (mod p, mod n, BN254 p)
     OPC_BN_REDC = 6, // BN254 Montgomery reduction (one per fq_mul / fq_mul2 / fq_dot)
+    OPC_FE_DOT = 7,  // secp256k1 a*b + c*d with one reduction (fe9_dot: 162 + 19 mads)
     OPC_N = 8
 };
 }  // namespace gsv

@@ -140,11 +140,13 @@ def fe9_case(rng, ma, mb, extreme):
     return a, b
 
 
-def run_fe9(lines, a, b, c=None):
+def run_fe9(lines, a, b, c=None, d=None):
     ops = {18 + i: a[i] for i in range(9)}
     ops.update({27 + j: b[j] for j in range(9)})
     if c is not None:
         ops.update({39 + j: c[j] for j in range(9)})
+    if d is not None:
+        ops.update({48 + j: d[j] for j in range(9)})
     ops.update({36: 31264, 37: 256, 38: 977})
     m = Machine(ops)
     m.run(lines)
@@ -205,6 +207,46 @@ def test_fe9_sqr_add_asm(ma):
         a2 = [x << 1 for x in a]
         c = addend_case(rng, extreme=(it < 2))
         check_weak(run_fe9(lines, a, a2, c), limbs_val(a) ** 2 + limbs_val(c))
+
+
+@pytest.mark.parametrize("m", [(1.04, 3.04, 1.04, 3), (1, 3.5, 1, 3.5), (1.04, 1.04, 2.64, 2.2)])
+def test_fe9_dot_asm(m):
+    """a*b + c*d with one reduction at m_a m_b + m_c m_d <= 7 (the mixed add's Y3: rr (V - X3) + Y1 (-2J))"""
+    ma, mb, mc, md = m
+    rng = random.Random(int(sum(m) * 1000))
+    lines = gen_fe9_asm.full_lines(gen_fe9_asm.DOT_TERMS)
+    for it in range(150):
+        a, b = fe9_case(rng, ma, mb, extreme=(it == 0))
+        c, d = fe9_case(rng, mc, md, extreme=(it == 0))
+        check_weak(run_fe9(lines, a, b, c, d), limbs_val(a) * limbs_val(b) + limbs_val(c) * limbs_val(d))
+
+
+def _q_consts():
+    """FE9_Q[M] limbs from fe9_q_consts.inc (Q_1..Q_7)"""
+    src = open(os.path.join(ROOT, "geth-sharding_amd", "csrc", "fe9_q_consts.inc")).read()
+    rows = [r for r in src.split("\n") if r.strip().startswith("{")]
+    return {m + 1: [int(x.strip().rstrip("u"), 16) for x in rows[m].strip().strip("{},").split(",")] for m in range(7)}
+
+
+def test_fe9_dot_asm_at_the_mixed_add_operands():
+    """the operands fe9_dot actually gets in gej9_add_ge_core, at their largest limbs: rr and Y1 are
+    product outputs (limb 2 up to 2^29 + 2^24), V - X3 = V + (Q_1 - X3), -2J = Q_2 - J - J (limb 8
+    near 2^30, far above a product output's 2^24)"""
+    Q = _q_consts()
+    prod = [(1 << 29) - 1] * 9
+    prod[2] = (1 << 29) + (1 << 24) - 1
+    prod[8] = (1 << 24) - 1
+    t = [prod[i] + Q[1][i] for i in range(9)]      # V - X3 with X3 = 0
+    w = list(Q[2])                                 # -2J with J = 0
+    lines = gen_fe9_asm.full_lines(gen_fe9_asm.DOT_TERMS)
+    check_weak(run_fe9(lines, prod, t, prod, w), limbs_val(prod) * limbs_val(t) + limbs_val(prod) * limbs_val(w))
+    rng = random.Random(99)
+    for _ in range(200):
+        a = [rng.randrange(x + 1) for x in prod]
+        c = [rng.randrange(x + 1) for x in prod]
+        b = [rng.randrange(x + 1) for x in t]
+        d = [rng.randrange(x + 1) for x in w]
+        check_weak(run_fe9(lines, a, b, c, d), limbs_val(a) * limbs_val(b) + limbs_val(c) * limbs_val(d))
 
 
 # --------------------------------------------------------------------------- BN254 REDC

@@ -31,7 +31,7 @@ import torch  # noqa: E402
 import gsv  # noqa: E402
 from gsv import _lib  # noqa: E402
 
-KINDS = ["fe_mul", "fe_sqr", "sc_mul", "sc_sqr", "bn_mul", "modinv", "bn_redc"]
+KINDS = ["fe_mul", "fe_sqr", "sc_mul", "sc_sqr", "bn_mul", "modinv", "bn_redc", "fe_dot"]
 
 
 def read(tu):
@@ -48,7 +48,7 @@ def per_unit(c, n):
 def main():
     ctx = gsv.Context(0)
     dev = torch.device("cuda", 0)
-    W = {"fe_mul": 100, "fe_sqr": 64, "sc_mul": 64, "sc_sqr": 36, "bn_mul": 81, "bn_redc": 81}
+    W = {"fe_mul": 100, "fe_sqr": 64, "sc_mul": 64, "sc_sqr": 36, "bn_mul": 81, "bn_redc": 81, "fe_dot": 181}
     out = {"build": "variants/opcount (-DGSV_OPCOUNT)", "unit": "v_mad_u64_u32 per unit of work",
            "weights_mad_per_op": W}
     # ---- configs[1]: 2^20 recoveries
@@ -65,7 +65,7 @@ def main():
     torch.cuda.synchronize()
     assert int(st.max()) == 0
     c = per_unit(read("ecrecover"), n)
-    c["mac_equiv"] = round(sum(W[k] * c.get(k, 0) for k in ("fe_mul", "fe_sqr", "sc_mul", "sc_sqr")), 1)
+    c["mac_equiv"] = round(sum(W[k] * c.get(k, 0) for k in ("fe_mul", "fe_sqr", "sc_mul", "sc_sqr", "fe_dot")), 1)
     out["recovery"] = c
     # ---- configs[4]: 4-pair checks, one GPU's batch and the 8-rank per-rank batch
     for name, nchk in (("pairing_check", 65536), ("pairing_check_8192", 8192)):

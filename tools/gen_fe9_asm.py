@@ -19,16 +19,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "geth-sharding_amd", "csrc", "fe9_asm.cuh")
 
 
-def full(name, doc, terms_of_column, addend=False):
+def full(name, doc, terms_of_column, addend=False, dot=False):
     L = full_lines(terms_of_column, addend)
     outs = ", ".join([f'"=&v"(r[{i}])' for i in range(9)] + [f'"=&v"(hi[{i}])' for i in range(8)] + ['"=&s"(sd)'])
     ins = ", ".join([f'"v"(a[{i}])' for i in range(9)] + [f'"v"(b[{j}])' for j in range(9)] +
                     ['"s"(k31264)', '"s"(k256)', '"s"(k977)'] +
-                    ([f'"v"(c[{j}])' for j in range(9)] if addend else []))
+                    ([f'"v"(c[{j}])' for j in range(9)] if addend or dot else []) +
+                    ([f'"v"(d[{j}])' for j in range(9)] if dot else []))
     body = "\\n\\t".join(L)
     return [f"// {doc}",
             f"__device__ __forceinline__ void {name}(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]"
-            + (", const uint32_t c[9]" if addend else "") + ") {",
+            + (", const uint32_t c[9]" if addend or dot else "") + (", const uint32_t d[9]" if dot else "") + ") {",
             "    uint32_t hi[8];",
             "    uint64_t sd;",
             "    uint32_t k31264 = 31264u, k256 = 256u, k977 = 977u;",
@@ -40,6 +41,11 @@ def full(name, doc, terms_of_column, addend=False):
 
 
 MUL_TERMS = lambda k: [(i, 9 + (k - i)) for i in range(9) if 0 <= k - i < 9]
+
+
+def DOT_TERMS(k):
+    """a b + c d: both products' terms in one column chain (one reduction for the two)"""
+    return MUL_TERMS(k) + [(18 + i, 27 + (k - i)) for i in range(9) if 0 <= k - i < 9]
 
 
 def SQR_TERMS(k):
@@ -58,6 +64,8 @@ def full_lines(terms_of_column, addend=False):
     a three-operand add, no further instruction).  Fixed pairs: C = v[2:3] (columns, then o17, then
     T), D = v[4:5] (the reduction's running value)."""
     cj = lambda j: f"%{39 + j}"
+    # term operand numbering: 0..8 a, 9..17 b, 18..26 c (%39..), 27..35 d (%48..; fe9_dot only)
+    opnd = lambda x: f"%{18 + x}" if x < 18 else f"%{39 + (x - 18)}"
     C, c0, c1 = "v[2:3]", "v2", "v3"
     D, d0, d1 = "v[4:5]", "v4", "v5"
     o = lambda k: f"%{k}" if k < 9 else f"%{k}"
@@ -71,9 +79,7 @@ def full_lines(terms_of_column, addend=False):
             L.append(f"v_lshrrev_b64 {C}, 29, {C}")
             first = False
         for (x, y) in terms_of_column(k):
-            xa = a(x)
-            yb = b(y - 9) if y >= 9 else a(y)
-            L.append(f"v_mad_u64_u32 {C}, {SD}, {xa}, {yb}, {'0' if first else C}")
+            L.append(f"v_mad_u64_u32 {C}, {SD}, {opnd(x)}, {opnd(y)}, {'0' if first else C}")
             first = False
         L.append(f"v_and_b32_e32 {o(k)}, 0x1fffffff, {c0}")
     L.append(f"v_lshrrev_b64 {C}, 29, {C}")               # o17 < 2^35
@@ -132,6 +138,7 @@ def main():
     out += full("fe9_mul_add_full", "r = a * b + c mod p, c limbs < 2^31 (fe9_mul_add's contract)", MUL_TERMS, True)
     out += full("fe9_sqr_add_full", "r = a^2 + c mod p with b = 2a limb-wise, c limbs < 2^31 (fe9_sqr_add's contract)",
                 SQR_TERMS, True)
+    out += full("fe9_dot_full", "r = a * b + c * d mod p, one reduction (fe9_dot's contract)", DOT_TERMS, dot=True)
     out.append("}  // namespace gsv")
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")
