@@ -397,30 +397,19 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     // by mixed adds of D = 2R' with their z-ratios zr_e, stored unscaled, then every entry below the
     // last rescaled to the last one's Z by the product of the later z-ratios.  A Jacobian result
     // (X, Y, Z) on E'' is (X, Y, Z zfac) on E.
+    // Built with co-Z arithmetic (secp256k1_fe9.cuh ge9_dblu / ge9_zaddu): the pair (2R, R) at the
+    // common Z = 2y, then each P_e = D + P_{e-1} keeps D co-Z with it; z-ratios as above.
     fe9 zfac;
     {
-        gej9 R1;
-        R1.x = x;
-        R1.y = y;
-        fe9_set_u32(R1.z, 1);
-        gej9 D;
-        gej9_dbl(D, R1);
-        fe9 u2, u3;
-        fe9_sqr(u2, D.z);  // 2*2 -> 1
-        fe9_mul(u3, u2, D.z);
-        ge9 Dp;
-        Dp.x = D.x;
-        Dp.y = D.y;
-        gej9 P;
-        fe9_mul(P.x, x, u2);
-        fe9_mul(P.y, y, u3);
-        fe9_set_u32(P.z, 1);
+        ge9 Dp, P;
+        fe9 zd;
+        ge9_dblu(Dp, P, zd, x, y);
         fe9 zr[GLV_NT];
 #pragma unroll
         for (int e = 0; e < GLV_NT; e++) {
             if (e) {
-                gej9 Pn;
-                gej9_add_ge_zr(Pn, zr[e], P, Dp);
+                ge9 Pn;
+                ge9_zaddu(Pn, Dp, zr[e], P);
                 P = Pn;
             }
 #pragma unroll
@@ -439,9 +428,9 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             scale_xy9(q, ex, ey, f);
 #pragma unroll
             for (int k = 0; k < 9; k++) GLV_SET(e, k, q.x.v[k], q.y.v[k]);
-            if (e) fe9_mul(f, f, zr[e]);  // 2*2 -> 1
+            if (e) fe9_mul(f, f, zr[e]);  // 1
         }
-        fe9_mul(zfac, D.z, P.z);  // 2*2 -> 1
+        fe9_mul(zfac, f, zd);  // f = all the z-ratios: the entries' common Z on E is zd f
     }
 #if GSV_GLV_BETA_TAB
     uint32_t ptabB[9 * GLV_NT];  // beta x_e
