@@ -45,6 +45,11 @@ MI30_CONST modinfo30 MI30_BN = {{0x187CFD47, 0x3082305B, 0x071CA8D3, 0x205AA45A,
 
 constexpr int32_t MI30_M30 = 0x3FFFFFFF;
 
+// 1: variable-time divsteps (mi30_divsteps_var), 0: the constant-time 600 fixed divsteps
+#ifndef MI30_VAR
+#define MI30_VAR 0
+#endif
+
 struct trans2x2 { int32_t u, v, q, r; };
 
 // 30 divsteps on the low limbs of f (odd) and g; returns the new zeta = -(delta + 1/2)
@@ -72,6 +77,58 @@ MI30_FN int32_t mi30_divsteps(int32_t zeta, uint32_t f0, uint32_t g0, trans2x2& 
     t.q = (int32_t)q;
     t.r = (int32_t)r;
     return zeta;
+}
+
+// The variable-time form (Bernstein-Yang's divstep with eta = -delta, as libsecp256k1's later
+// modinv32_var): a run of zero low bits of g is one shift (count trailing zeros), and each odd step
+// clears up to 8 more bits at once with w = -g f^-1 mod 2^limit.  The 30-step transition matrix is
+// the same kind of matrix (|u| + |v| <= 2^30 ...), so update_de / update_fg apply unchanged.  Nothing
+// here is secret (signatures and public keys are public), so data-dependent timing is harmless; on
+// the GPU a wave runs as many inner iterations as its slowest lane (~12 per 30 divsteps instead of
+// 30 fixed steps).
+#if defined(__HIPCC__)
+#define MI30_CTZ(x) ((uint32_t)__builtin_ctz(x))
+#define MI30_MUL8(a, b) __umul24((a), (b))  /* only the low 8 bits of the product are used */
+#define MI30_ANY(x) (__any(x) != 0)
+#else
+#define MI30_CTZ(x) ((uint32_t)__builtin_ctz(x))
+#define MI30_MUL8(a, b) ((a) * (b))
+#define MI30_ANY(x) (x)
+#endif
+MI30_FN int32_t mi30_divsteps_var(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
+    uint32_t u = 1, v = 0, q = 0, r = 1, f = f0, g = g0;
+    int32_t i = 30;
+    for (;;) {
+        uint32_t zeros = MI30_CTZ(g | (0xFFFFFFFFu << i));  // <= i
+        g >>= zeros;
+        u <<= zeros;
+        v <<= zeros;
+        eta -= (int32_t)zeros;
+        i -= (int32_t)zeros;
+        if (i == 0) break;
+        if (eta < 0) {  // g odd and eta < 0: (f, g) <- (g, -f), (u, q) <- (q, -u), (v, r) <- (r, -v)
+            uint32_t x;
+            eta = -eta;
+            x = f; f = g; g = 0u - x;
+            x = u; u = q; q = 0u - x;
+            x = v; v = r; r = 0u - x;
+        }
+        int32_t limit = (eta + 1) > i ? i : (eta + 1);
+        uint32_t m = (0xFFFFFFFFu >> (32 - limit)) & 255u;
+        // f^-1 mod 256 by Newton from f (correct mod 8 for odd f): two steps give mod 2^12
+        uint32_t fl = f & 255u, x = fl;
+        x = MI30_MUL8(x, 2u - MI30_MUL8(fl, x)) & 255u;
+        x = MI30_MUL8(x, 2u - MI30_MUL8(fl, x)) & 255u;
+        uint32_t w = (0u - MI30_MUL8(g & 255u, x)) & m;  // g + f w == 0 mod 2^limit
+        g = (uint32_t)((uint64_t)f * w + g);
+        q = (uint32_t)((uint64_t)u * w + q);
+        r = (uint32_t)((uint64_t)v * w + r);
+    }
+    t.u = (int32_t)u;
+    t.v = (int32_t)v;
+    t.q = (int32_t)q;
+    t.r = (int32_t)r;
+    return eta;
 }
 
 // [d, e] <- t [d, e] / 2^30 (mod m), keeping d, e in (-2m, m)
@@ -185,6 +242,25 @@ MI30_FN void modinv30_words(uint32_t out[8], const uint32_t x[8], const modinfo3
     }
     e.v[0] = 1;
     s30_from_words(g, x);
+#if MI30_VAR
+    // variable-time divsteps until g == 0 in every lane of the wave (a lane that is done keeps
+    // d and f: its matrix is then diag(2^30, 1)); 25 batches cover the original divstep's bound
+    // for 256-bit inputs (724), ~19 are typical
+    int32_t eta = -1;
+#if defined(__HIPCC__)
+#pragma unroll 1
+#endif
+    for (int it = 0; it < 25; it++) {
+        trans2x2 t;
+        eta = mi30_divsteps_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+        mi30_update_de(d, e, t, mi);
+        mi30_update_fg(f, g, t);
+        uint32_t gz = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) gz |= (uint32_t)g.v[k];
+        if (!MI30_ANY(gz != 0)) break;
+    }
+#else
     int32_t zeta = -1;
 #if defined(__HIPCC__)
 #pragma unroll 1
@@ -195,6 +271,7 @@ MI30_FN void modinv30_words(uint32_t out[8], const uint32_t x[8], const modinfo3
         mi30_update_de(d, e, t, mi);
         mi30_update_fg(f, g, t);
     }
+#endif
     mi30_normalize(d, f.v[8], mi);
     s30_to_words(out, d);
 }
