@@ -23,10 +23,11 @@ SANITIZE_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,un
                   "-fno-sanitize-recover=undefined"] if os.environ.get("GSV_SANITIZE") == "1" else []
 
 
-def build_native(src, out, std="c++17"):
+def build_native(src, out, std="c++17", defines=()):
     """g++ -shared of tests/native/<src> (plus the sanitizer flags when GSV_SANITIZE=1)."""
     import subprocess
     subprocess.run(["g++", "-O2", f"-std={std}", "-shared", "-fPIC", "-Wno-unknown-pragmas"] + SANITIZE_FLAGS +
+                   [f"-D{d}" for d in defines] +
                    ["-o", str(out), os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", src)],
                    check=True)
     import ctypes

@@ -293,8 +293,18 @@ N_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 BN_P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
 
 
-def test_safegcd_modinv(lib):
-    """modinv30.cuh (Bernstein-Yang divsteps) against pow(x, -1, m) for m = n, p and the BN254 prime."""
+@pytest.fixture(scope="module", params=[0, 1], ids=["const-time", "var-time"])
+def inv_lib(request, tmp_path_factory):
+    """the host harness built with each divstep form (modinv30.cuh MI30_VAR)"""
+    from conftest import build_native
+    return build_native("fe9_host.cpp", tmp_path_factory.mktemp("fe9v") / f"fe9_host_v{request.param}.so",
+                        defines=[f"MI30_VAR={request.param}"])
+
+
+def test_safegcd_modinv(inv_lib):
+    """modinv30.cuh (Bernstein-Yang divsteps, constant- and variable-time) against pow(x, -1, m) for
+    m = n, p and the BN254 prime."""
+    lib = inv_lib
     rng = random.Random(20)
     W8 = ctypes.c_uint32 * 8
     for which, m in ((0, N_ORDER), (1, P), (2, BN_P)):
