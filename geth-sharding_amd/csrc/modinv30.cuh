@@ -45,9 +45,10 @@ MI30_CONST modinfo30 MI30_BN = {{0x187CFD47, 0x3082305B, 0x071CA8D3, 0x205AA45A,
 
 constexpr int32_t MI30_M30 = 0x3FFFFFFF;
 
-// 1: variable-time divsteps (mi30_divsteps_var), 0: the constant-time 600 fixed divsteps
+// 1: variable-time divsteps (mi30_divsteps_var; +0.95 % on ecrecover, profiles/r02/ab_vargcd.txt),
+// 0: the constant-time 600 fixed divsteps
 #ifndef MI30_VAR
-#define MI30_VAR 0
+#define MI30_VAR 1
 #endif
 
 struct trans2x2 { int32_t u, v, q, r; };
