@@ -44,7 +44,9 @@ struct Layout {
     }
 };
 
-enum ShapeKind : uint64_t { SK_CHUNK = 1, SK_PAIRING = 2, SK_NOTARY = 3, SK_DERIVE = 4, SK_POC = 5, SK_HEADER = 6 };
+enum ShapeKind : uint64_t {
+    SK_CHUNK = 1, SK_PAIRING = 2, SK_NOTARY = 3, SK_DERIVE = 4, SK_POC = 5, SK_HEADER = 6, SK_PARTITION = 7
+};
 
 // scatter run: roots of group positions [from, from + count) go to output indices [dst, dst + count)
 struct Run { uint32_t dst, from, count; };
@@ -103,6 +105,10 @@ struct Shape {
     uint32_t salt_len = 0;
     // SK_HEADER
     size_t o_hscr = 0;
+    // SK_PARTITION (+ the SK_NOTARY fields of the rank's own block)
+    size_t p_n = 0, p_total = 0;
+    int p_ranks = 1, p_rank = 0;
+    size_t o_lroot = 0, o_lntx = 0, o_lbm = 0, o_block = 0, o_all = 0;
 
     Shape() = default;
     Shape(const Shape&) = delete;
@@ -1089,6 +1095,72 @@ int header_shape(gsv_ctx*, Shape& s, size_t n, Layout& L) {
     return GSV_SUCCESS;
 }
 
+// ---- shard partition: the notary shape of this rank's block + its record block and the gathered
+// blocks; key = notary key of the block + (n_total, nranks, rank)
+struct PartDims {
+    size_t first, n, per, R, bm, B;
+};
+PartDims part_dims(size_t n_total, int N, int r, uint32_t max_txs) {
+    PartDims d;
+    d.first = n_total * (size_t)r / (size_t)N;
+    d.n = n_total * (size_t)(r + 1) / (size_t)N - d.first;
+    d.per = (n_total + N - 1) / N;
+    d.bm = (max_txs + 7) / 8;
+    d.R = (36 + d.bm + 7) / 8 * 8;  // root 32 | ntx 4 | bitmap, padded to 8 (gsv/shards.py)
+    d.B = 8 + d.per * d.R;          // header {int32 status, uint32 shards} + records
+    return d;
+}
+std::vector<uint64_t> partition_key(const uint64_t* h_off, size_t n, size_t n_total, int N, int r, const uint8_t* cid,
+                                    size_t cidlen, int signer, uint32_t max_txs) {
+    std::vector<uint64_t> k = notary_key(h_off, n, cid, cidlen, signer, max_txs);
+    k.push_back(n_total);
+    k.push_back((uint64_t)N);
+    k.push_back((uint64_t)r);
+    return k;
+}
+int partition_shape(gsv_ctx* c, Shape& s, const uint64_t* h_off, size_t n_total, int N, int r, const uint8_t* cid,
+                    size_t cidlen, int signer_kind, uint32_t max_txs, Layout& L) {
+    PartDims d = part_dims(n_total, N, r, max_txs);
+    if (d.n) {
+        int rc = notary_shape(c, s, h_off, h_off + 1, d.n, cid, cidlen, signer_kind, max_txs, L);
+        if (rc) return rc;
+    }
+    s.kind = SK_PARTITION;
+    s.max_txs = max_txs;
+    s.p_n = d.n;
+    s.p_total = n_total;
+    s.p_ranks = N;
+    s.p_rank = r;
+    s.o_lroot = L.add(d.n * 32);
+    s.o_lntx = L.add(d.n * 4);
+    s.o_lbm = L.add(d.n * d.bm);
+    s.o_block = L.add(d.B);
+    s.o_all = L.add((size_t)N * d.B);
+    return GSV_SUCCESS;
+}
+// validate the rank's block and pack its records into `blk`
+int partition_pack(gsv_ctx* c, const Shape& s, const PartDims& d, const uint8_t* d_bodies, uint8_t* d_senders,
+                   uint8_t* d_status, uint8_t* blk, hipStream_t st) {
+    uint8_t* lroot = s.at<uint8_t>(s.o_lroot);
+    uint32_t* lntx = s.at<uint32_t>(s.o_lntx);
+    uint8_t* lbm = s.at<uint8_t>(s.o_lbm);
+    if (d.n) {
+        int rc = notary_run(c, s, d.n, d_bodies, lroot, lntx, lbm, d_senders, d_status, st);
+        if (rc) return rc;
+    }
+    return hip_err(gsv::launch_partition_pack(lroot, lntx, lbm, (uint32_t)d.n, (uint32_t)d.per, (uint32_t)d.R,
+                                              (uint32_t)d.bm, 0, blk, st));
+}
+// the path's one collective: every rank's block to every rank (one ncclAllGather over xGMI)
+int partition_gather(gsv_ctx* c, const uint8_t* blk, uint8_t* all, const PartDims& d, hipStream_t st) {
+    if (c->nranks > 1 && c->comm) {
+        if (ncclAllGather(blk, all, d.B, ncclUint8, c->comm, st) != ncclSuccess) return GSV_E_RCCL;
+        return GSV_SUCCESS;
+    }
+    if (c->nranks > 1) return GSV_E_INVALID_ARG;
+    return hip_err(hipMemcpyAsync(all, blk, d.B, hipMemcpyDeviceToDevice, st));
+}
+
 // Prepare-or-find: returns the cached shape for (kind, key), building it with `build` on a miss.
 template <typename B>
 int shape_get(gsv_ctx* c, uint64_t kind, std::vector<uint64_t>&& key, B&& build, Shape** out) {
@@ -1501,79 +1573,197 @@ int gsv_shard_range(size_t n_shards, int nranks, int rank, size_t* first, size_t
     return GSV_SUCCESS;
 }
 
+size_t gsv_partition_block_bytes(size_t n_total, int nranks, uint32_t max_txs) {
+    if (nranks < 1) return 0;
+    return part_dims(n_total, nranks, 0, max_txs).B;
+}
+
+int gsv_notary_partition_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n_total, int nranks, int rank,
+                                 const uint8_t* chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs) {
+    if (!c || !h_off || nranks < 1 || rank < 0 || rank >= nranks) return GSV_E_INVALID_ARG;
+    int rc = notary_args(chain_id, chain_id_len, signer_kind, n_total, max_txs);
+    if (rc) return rc;
+    if (n_total > 0xFFFFFFFFull / 4096) return GSV_E_TOO_LARGE;
+    PartDims d = part_dims(n_total, nranks, rank, max_txs);
+    std::lock_guard<std::mutex> g(c->smu);
+    HIPCHK(hipSetDevice(c->device));
+    Shape* s;
+    return shape_get(c, SK_PARTITION,
+                     partition_key(h_off, d.n, n_total, nranks, rank, chain_id, chain_id_len, signer_kind, max_txs),
+                     [&](Shape& ns, Layout& L) {
+                         return partition_shape(c, ns, h_off, n_total, nranks, rank, chain_id, chain_id_len,
+                                                signer_kind, max_txs, L);
+                     },
+                     &s);
+}
+
+int gsv_notary_partition_pack_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n_total,
+                                  int nranks, int rank, const uint8_t* chain_id, size_t chain_id_len, int signer_kind,
+                                  uint32_t max_txs, uint8_t* d_block, uint8_t* d_senders, uint8_t* d_status,
+                                  void* stream) {
+    if (!c || !h_off || !d_block || nranks < 1 || rank < 0 || rank >= nranks) return GSV_E_INVALID_ARG;
+    int rc = notary_args(chain_id, chain_id_len, signer_kind, n_total, max_txs);
+    if (rc) return rc;
+    PartDims d = part_dims(n_total, nranks, rank, max_txs);
+    if (d.n && !d_bodies) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->smu);
+    Shape* s = shape_find(c, SK_PARTITION,
+                          partition_key(h_off, d.n, n_total, nranks, rank, chain_id, chain_id_len, signer_kind, max_txs));
+    if (!s) return GSV_E_NOT_PREPARED;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return shape_run(c, *s, st, [&] { return partition_pack(c, *s, d, d_bodies, d_senders, d_status, d_block, st); });
+}
+
+int gsv_notary_partition_unpack_dev(gsv_ctx* c, const uint8_t* d_blocks, size_t n_total, int nranks, uint32_t max_txs,
+                                    uint8_t* d_root32_all, uint32_t* d_ntx_all, uint8_t* d_bitmap_all,
+                                    int32_t* d_rank_status, void* stream) {
+    if (!c || !d_blocks || nranks < 1 || max_txs == 0 || (n_total && (!d_root32_all || !d_ntx_all || !d_bitmap_all)))
+        return GSV_E_INVALID_ARG;
+    if (n_total > 0xFFFFFFFFull / 4096) return GSV_E_TOO_LARGE;
+    PartDims d = part_dims(n_total, nranks, 0, max_txs);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return hip_err(gsv::launch_partition_unpack(d_blocks, (uint32_t)nranks, (uint32_t)n_total, (uint32_t)d.R,
+                                                (uint32_t)d.bm, d.B, d_root32_all, d_ntx_all, d_bitmap_all,
+                                                d_rank_status, st));
+}
+
+int gsv_notary_validate_partition_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n_total,
+                                      const uint8_t* chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
+                                      uint8_t* d_root32_all, uint32_t* d_ntx_all, uint8_t* d_bitmap_all,
+                                      uint8_t* d_senders, uint8_t* d_status, int32_t* d_rank_status, void* stream) {
+    // arguments every rank passes alike: an error here is the same error on every rank, and no rank
+    // enters the collective
+    if (!c || (n_total && (!d_root32_all || !d_ntx_all || !d_bitmap_all))) return GSV_E_INVALID_ARG;
+    int rc = notary_args(chain_id, chain_id_len, signer_kind, n_total, max_txs);
+    if (rc || n_total == 0) return rc;
+    if (n_total > 0xFFFFFFFFull / 4096) return GSV_E_TOO_LARGE;
+    const int N = c->nranks, r = c->rank;
+    PartDims d = part_dims(n_total, N, r, max_txs);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    // rank-local failures still reach the all-gather with the rank's status in its block header
+    int lrc = (!h_off || (d.n && !d_bodies)) ? GSV_E_INVALID_ARG : GSV_SUCCESS;
+    bool joined = false;  // this rank has entered the all-gather
+    if (!lrc) {
+        std::lock_guard<std::mutex> g(c->smu);
+        Shape* s = shape_find(c, SK_PARTITION, partition_key(h_off, d.n, n_total, N, r, chain_id, chain_id_len,
+                                                             signer_kind, max_txs));
+        if (!s) lrc = GSV_E_NOT_PREPARED;
+        else if (hipSetDevice(c->device) != hipSuccess) lrc = GSV_E_HIP;
+        else {
+            lrc = shape_run(c, *s, st, [&] {
+                uint8_t* blk = s->at<uint8_t>(s->o_block);
+                uint8_t* all = s->at<uint8_t>(s->o_all);
+                int e = partition_pack(c, *s, d, d_bodies, d_senders, d_status, blk, st);
+                if (e) return e;
+                joined = true;
+                e = partition_gather(c, blk, all, d, st);
+                if (e) return e;
+                return hip_err(gsv::launch_partition_unpack(all, (uint32_t)N, (uint32_t)n_total, (uint32_t)d.R,
+                                                            (uint32_t)d.bm, d.B, d_root32_all, d_ntx_all,
+                                                            d_bitmap_all, d_rank_status, st));
+            });
+            if (!lrc || joined) return lrc;  // done, or failed at/after the collective: nothing more to join
+        }
+    }
+    // error path: join the collective from the staging arena with this rank's status and no records
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return lrc;
+    if (arena_reserve(c, al(d.B) + al((size_t)N * d.B))) return lrc;
+    uint8_t* blk = c->arena;
+    uint8_t* all = c->arena + al(d.B);
+    if (gsv::launch_partition_pack(nullptr, nullptr, nullptr, 0, (uint32_t)d.per, (uint32_t)d.R, (uint32_t)d.bm, lrc,
+                                   blk, st) != hipSuccess)
+        return lrc;
+    if (partition_gather(c, blk, all, d, st)) return lrc;
+    gsv::launch_partition_unpack(all, (uint32_t)N, (uint32_t)n_total, (uint32_t)d.R, (uint32_t)d.bm, d.B,
+                                 d_root32_all, d_ntx_all, d_bitmap_all, d_rank_status, st);
+    hipStreamSynchronize(st);  // the arena is reused by the next host-path call
+    return lrc;
+}
+
 int gsv_notary_validate_partition(gsv_ctx* c, const uint8_t* bodies, const uint64_t* off, size_t n_total,
                                   const uint8_t* chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
                                   uint8_t* root32_all, uint32_t* ntx_all, uint8_t* bitmap_all,
                                   uint8_t* senders_out, uint8_t* status_out) {
+    // arguments every rank passes alike (see the _dev form)
     if (!c || !off || (n_total && (!root32_all || !ntx_all || !bitmap_all))) return GSV_E_INVALID_ARG;
-    const int N = c->nranks, r = c->rank;
-    size_t first = 0, n = 0;
-    gsv_shard_range(n_total, N, r, &first, &n);
     int rc = notary_args(chain_id, chain_id_len, signer_kind, n_total, max_txs);
     if (rc || n_total == 0) return rc;
-    if (n && !bodies) return GSV_E_INVALID_ARG;
-    for (size_t i = 0; i < n; i++)
-        if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_BODY) return GSV_E_TOO_LARGE;
-    const size_t bm = (max_txs + 7) / 8, R = (36 + bm + 7) / 8 * 8, per = (n_total + N - 1) / N;
-    const size_t nt = n * (size_t)max_txs;
+    if (n_total > 0xFFFFFFFFull / 4096) return GSV_E_TOO_LARGE;
+    const int N = c->nranks, r = c->rank;
+    PartDims d = part_dims(n_total, N, r, max_txs);
+    const size_t n = d.n, nt = n * (size_t)max_txs;
     std::lock_guard<std::mutex> g(c->mu);
     std::lock_guard<std::mutex> g2(c->smu);
     HIPCHK(hipSetDevice(c->device));
+    hipStream_t sm = c->stream;
+    // gathered outputs + statuses first in the arena, so the error path finds them at the same place
+    const size_t out_bytes = al(d.B) + al((size_t)N * d.B) + al(n_total * 32) + al(n_total * 4) +
+                             al(n_total * d.bm) + al((size_t)N * 4);
+    int lrc = (n && !bodies) ? GSV_E_INVALID_ARG : GSV_SUCCESS;
+    for (size_t i = 0; i < n && !lrc; i++)
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > MAX_BODY) lrc = GSV_E_TOO_LARGE;
     std::vector<uint64_t> st, en;
     uint64_t pos = n ? stage_offsets(off, n, st, en) : 0;
-    size_t staged = al(pos + 16) + al(n * 32 + 1) + al(n * 4 + 1) + al(n * bm + 1) + al(nt * 20 + 1) + al(nt + 1) +
-                    al(per * R) + al((size_t)N * per * R);
+    size_t staged = out_bytes + al(pos + 16) + al(n * 32 + 1) + al(n * 4 + 1) + al(n * d.bm + 1) + al(nt * 20 + 1) +
+                    al(nt + 1);
     Shape s;
-    if (n) {
-        rc = shape_temp(c, staged,
-                        [&](Shape& ns, Layout& L) {
-                            return notary_shape(c, ns, st.data(), en.data(), n, chain_id, chain_id_len, signer_kind,
-                                                max_txs, L);
-                        },
-                        s);
-    } else {
-        rc = arena_reserve(c, staged);
+    if (!lrc) {
+        lrc = shape_temp(c, staged,
+                         [&](Shape& ns, Layout& L) {
+                             if (!n) return GSV_SUCCESS;
+                             return notary_shape(c, ns, st.data(), en.data(), n, chain_id, chain_id_len, signer_kind,
+                                                 max_txs, L);
+                         },
+                         s);
     }
-    if (rc) return rc;
+    if (lrc && arena_reserve(c, out_bytes)) return lrc;  // cannot even join the collective
     Carve cv(c->arena);
-    uint8_t* d_b = cv.take<uint8_t>(pos + 16);
-    uint8_t* d_r = cv.take<uint8_t>(n * 32 + 1);
-    uint32_t* d_n = cv.take<uint32_t>(n * 4 + 1);
-    uint8_t* d_bm = cv.take<uint8_t>(n * bm + 1);
-    uint8_t* d_snd = cv.take<uint8_t>(nt * 20 + 1);
-    uint8_t* d_st = cv.take<uint8_t>(nt + 1);
-    uint8_t* d_rec = cv.take<uint8_t>(per * R);
-    uint8_t* d_all = cv.take<uint8_t>((size_t)N * per * R);
-    hipStream_t sm = c->stream;
-    HIPCHK(hipMemsetAsync(d_rec, 0, per * R, sm));
-    if (n) {
-        rc = stage_bodies(c, d_b, bodies, off, n, st, en);
-        if (rc) return rc;
-        rc = shape_run(c, s, sm, [&] {
-            return notary_run(c, s, n, d_b, d_r, d_n, d_bm, senders_out ? d_snd : nullptr, status_out ? d_st : nullptr, sm);
-        });
-        if (rc) return rc;
-        HIPCHK(hipMemcpy2DAsync(d_rec, R, d_r, 32, 32, n, hipMemcpyDeviceToDevice, sm));
-        HIPCHK(hipMemcpy2DAsync(d_rec + 32, R, d_n, 4, 4, n, hipMemcpyDeviceToDevice, sm));
-        HIPCHK(hipMemcpy2DAsync(d_rec + 36, R, d_bm, bm, bm, n, hipMemcpyDeviceToDevice, sm));
+    uint8_t* d_blk = cv.take<uint8_t>(d.B);
+    uint8_t* d_all = cv.take<uint8_t>((size_t)N * d.B);
+    uint8_t* d_oroot = cv.take<uint8_t>(n_total * 32);
+    uint32_t* d_ontx = cv.take<uint32_t>(n_total * 4);
+    uint8_t* d_obm = cv.take<uint8_t>(n_total * d.bm);
+    int32_t* d_rst = cv.take<int32_t>((size_t)N * 4);
+    uint8_t* d_snd = nullptr;
+    uint8_t* d_st = nullptr;
+    if (!lrc) {
+        uint8_t* d_b = cv.take<uint8_t>(pos + 16);
+        uint8_t* d_r = cv.take<uint8_t>(n * 32 + 1);
+        uint32_t* d_n = cv.take<uint32_t>(n * 4 + 1);
+        uint8_t* d_bm = cv.take<uint8_t>(n * d.bm + 1);
+        d_snd = cv.take<uint8_t>(nt * 20 + 1);
+        d_st = cv.take<uint8_t>(nt + 1);
+        if (n) lrc = stage_bodies(c, d_b, bodies, off, n, st, en);
+        if (!lrc && n)
+            lrc = shape_run(c, s, sm, [&] {
+                return notary_run(c, s, n, d_b, d_r, d_n, d_bm, senders_out ? d_snd : nullptr,
+                                  status_out ? d_st : nullptr, sm);
+            });
+        if (!lrc)
+            lrc = hip_err(gsv::launch_partition_pack(d_r, d_n, d_bm, (uint32_t)n, (uint32_t)d.per, (uint32_t)d.R,
+                                                     (uint32_t)d.bm, 0, d_blk, sm));
     }
-    if (N > 1 && c->comm) {
-        if (ncclAllGather(d_rec, d_all, per * R, ncclUint8, c->comm, sm) != ncclSuccess) return GSV_E_RCCL;
-    } else {
-        HIPCHK(hipMemcpyAsync(d_all, d_rec, per * R, hipMemcpyDeviceToDevice, sm));
-    }
-    for (int q = 0; q < N; q++) {
-        size_t f = 0, k = 0;
-        gsv_shard_range(n_total, N, q, &f, &k);
-        if (!k) continue;
-        const uint8_t* src = d_all + (size_t)q * per * R;
-        HIPCHK(hipMemcpy2DAsync(root32_all + f * 32, 32, src, R, 32, k, hipMemcpyDeviceToHost, sm));
-        HIPCHK(hipMemcpy2DAsync(ntx_all + f, 4, src + 32, R, 4, k, hipMemcpyDeviceToHost, sm));
-        HIPCHK(hipMemcpy2DAsync(bitmap_all + f * bm, bm, src + 36, R, bm, k, hipMemcpyDeviceToHost, sm));
-    }
-    if (n && senders_out) HIPCHK(hipMemcpyAsync(senders_out, d_snd, nt * 20, hipMemcpyDeviceToHost, sm));
-    if (n && status_out) HIPCHK(hipMemcpyAsync(status_out, d_st, nt, hipMemcpyDeviceToHost, sm));
+    if (lrc && gsv::launch_partition_pack(nullptr, nullptr, nullptr, 0, (uint32_t)d.per, (uint32_t)d.R,
+                                          (uint32_t)d.bm, lrc, d_blk, sm) != hipSuccess)
+        return lrc;
+    int grc = partition_gather(c, d_blk, d_all, d, sm);
+    if (grc) return grc;
+    HIPCHK(gsv::launch_partition_unpack(d_all, (uint32_t)N, (uint32_t)n_total, (uint32_t)d.R, (uint32_t)d.bm, d.B,
+                                        d_oroot, d_ontx, d_obm, d_rst, sm));
+    std::vector<int32_t> rst(N);
+    HIPCHK(hipMemcpyAsync(root32_all, d_oroot, n_total * 32, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(ntx_all, d_ontx, n_total * 4, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(bitmap_all, d_obm, n_total * d.bm, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(rst.data(), d_rst, (size_t)N * 4, hipMemcpyDeviceToHost, sm));
+    if (!lrc && n && senders_out) HIPCHK(hipMemcpyAsync(senders_out, d_snd, nt * 20, hipMemcpyDeviceToHost, sm));
+    if (!lrc && n && status_out) HIPCHK(hipMemcpyAsync(status_out, d_st, nt, hipMemcpyDeviceToHost, sm));
     HIPCHK(hipStreamSynchronize(sm));
+    // every rank returns the same verdict: the status of the lowest failing rank
+    for (int q = 0; q < N; q++)
+        if (rst[q]) return rst[q];
     for (size_t i = 0; i < n_total; i++)
         if (ntx_all[i] > max_txs) return GSV_E_TOO_LARGE;
     return GSV_SUCCESS;

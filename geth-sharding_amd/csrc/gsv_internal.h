@@ -74,6 +74,12 @@ hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, u
 
 // notary.hip
 size_t blob_rec_bytes();
+hipError_t launch_partition_pack(const uint8_t* d_root, const uint32_t* d_ntx, const uint8_t* d_bm, uint32_t n,
+                                 uint32_t per, uint32_t R, uint32_t bm, int32_t status, uint8_t* d_block,
+                                 hipStream_t st);
+hipError_t launch_partition_unpack(const uint8_t* d_all, uint32_t nranks, uint32_t n_total, uint32_t R, uint32_t bm,
+                                   size_t B, uint8_t* d_root, uint32_t* d_ntx, uint8_t* d_bm, int32_t* d_rank_status,
+                                   hipStream_t st);
 hipError_t launch_blob_index(const uint8_t* d_bodies, const uint64_t* d_off, const uint32_t* d_len,
                              uint32_t n_shards, uint32_t max_txs, void* d_blobs, uint32_t* d_ntx, hipStream_t st);
 hipError_t launch_notary_tx(const uint8_t* d_bodies, const uint64_t* d_off, const void* d_blobs,

@@ -403,9 +403,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
 // Not on the validation path.  Shard `s`, tx j: EIP-155 transaction (chain id 1) signed with
 // key_(s,j); RLP-encoded (102-105 bytes) and blob-serialized into exactly 4 chunks at body offset
 // 128*j, so 8,192 txs fill a 2^20-byte body (sharding/utils/marshal.go:71-123 layout).
-// Every 128th tx (j % 128 == 127) is invalid by construction, cycling through: high-s
-// (ErrInvalidSig), wrong chain id (ErrInvalidChainId), r not an x-coordinate (ErrRecoverFailed).
-// Every encoding keeps r and s at 32 bytes, so each tx is 100-105 bytes = 4 chunks.
+// Every 128th tx (j % 128 == 127) is invalid by construction, class (gi / 128) % 4: high-s
+// (ErrInvalidSig), wrong chain id (ErrInvalidChainId), r not an x-coordinate (ErrRecoverFailed), and
+// recid flipped: a valid signature of ANOTHER key, so its status is OK and only the recovered sender
+// (!= the signer, whose address exp_sender holds) tells it apart.  The CPU
+// restatement with the reference's own signer is oracle/ref_shim.c gsvref_notary_synth_body.
+// Each tx is 94-124 bytes = 4 chunks.
 GSV_DI uint32_t put_be_min(uint8_t* o, uint64_t v) {  // minimal big-endian bytes, returns count
     uint32_t n = 0;
     for (int i = 7; i >= 0; i--) {
@@ -510,7 +513,7 @@ __global__ __launch_bounds__(256) void k_notary_synth(uint64_t seed, uint32_t sh
     ecdsa_sign(r, sg, recid, px, py, d, k, msg, gtab);
     uint32_t chain = 1, st = GSV_ST_OK;
     if (j % 128 == 127) {
-        uint32_t cls = (uint32_t)((gi / 128) % 3);
+        uint32_t cls = (uint32_t)((gi / 128) % 4);
         if (cls == 0) {  // high-s: n - s (still a valid signature; Homestead rule rejects it)
             sc t, u;
 #pragma unroll
@@ -523,10 +526,12 @@ __global__ __launch_bounds__(256) void k_notary_synth(uint64_t seed, uint32_t sh
         } else if (cls == 1) {  // signed for chain 1 but V encodes chain 5
             chain = 5;
             st = GSV_ST_INVALID_CHAIN_ID;
-        } else {  // r = 2^255 + 2: r^3 + 7 is a non-residue mod p, so no point has x = r (< n)
+        } else if (cls == 2) {  // r = 2^255 + 2: r^3 + 7 is a non-residue mod p, so no point has x = r (< n)
 #pragma unroll
             for (int i = 0; i < 8; i++) r[i] = i == 0 ? 2u : i == 7 ? 0x80000000u : 0u;
             st = GSV_ST_RECOVER_FAILED;
+        } else {  // recid flipped: R' = -R recovers r^-1 (s R' - m G) != the signer's key
+            recid ^= 1u;
         }
     }
     w += put_uint(body + w, (recid & 1u) + 35 + 2 * chain);
@@ -548,6 +553,70 @@ __global__ __launch_bounds__(256) void k_notary_synth(uint64_t seed, uint32_t sh
     }
     if (exp_status) exp_status[id] = (uint8_t)st;
     if (exp_sender) store_pub_addr(nullptr, exp_sender + (size_t)id * 20, st == GSV_ST_OK, px, py);
+}
+
+// ---------------------------------------------------------------- shard-partition records
+// One rank's block (gsv.h gsv_partition_block_bytes): header {int32 status, uint32 shards} then
+// `per` records of R bytes: root 32 | ntx 4 | bitmap bm | zero pad (the layout of gsv/shards.py).
+// A rank whose local validation failed packs its status and zero records, so every rank always
+// reaches the all-gather (sharding/node/backend.go:245-284 partition; one record set per shard).
+__global__ __launch_bounds__(256) void k_partition_pack(const uint8_t* __restrict__ root, const uint32_t* __restrict__ ntx,
+                                                        const uint8_t* __restrict__ bitmap, uint32_t n, uint32_t per,
+                                                        uint32_t R, uint32_t bm, int32_t status,
+                                                        uint8_t* __restrict__ block) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        *(int32_t*)block = status;
+        *(uint32_t*)(block + 4) = status ? 0u : n;
+    }
+    if (i >= per * R) return;
+    const uint32_t k = i / R, o = i % R;
+    uint8_t v = 0;
+    if (k < n && status == 0) {
+        if (o < 32) v = root[(size_t)k * 32 + o];
+        else if (o < 36) v = (uint8_t)(ntx[k] >> (8 * (o - 32)));
+        else if (o < 36 + bm) v = bitmap[(size_t)k * bm + (o - 36)];
+    }
+    block[8 + i] = v;
+}
+
+// all = nranks blocks of B bytes (rank order) -> per-shard outputs in shard order + rank statuses
+__global__ __launch_bounds__(256) void k_partition_unpack(const uint8_t* __restrict__ all, uint32_t nranks,
+                                                          uint32_t n_total, uint32_t R, uint32_t bm, size_t B,
+                                                          uint8_t* __restrict__ root, uint32_t* __restrict__ ntx,
+                                                          uint8_t* __restrict__ bitmap, int32_t* __restrict__ rank_status) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (rank_status && i < nranks) rank_status[i] = *(const int32_t*)(all + (size_t)i * B);
+    if (i >= n_total * R) return;
+    const uint32_t s = i / R, o = i % R;
+    // owner rank q: first(q) = floor(S q / N) <= s < first(q + 1)
+    uint32_t q = (uint32_t)(((uint64_t)s * nranks + nranks - 1) / n_total);
+    while (q > 0 && (uint64_t)n_total * q / nranks > s) q--;
+    while (q + 1 < nranks && (uint64_t)n_total * (q + 1) / nranks <= s) q++;
+    const uint32_t k = s - (uint32_t)((uint64_t)n_total * q / nranks);
+    const uint8_t* rec = all + (size_t)q * B + 8 + (size_t)k * R;
+    if (o < 32) root[(size_t)s * 32 + o] = rec[o];
+    else if (o == 32) ntx[s] = *(const uint32_t*)(rec + 32);
+    else if (o >= 36 && o < 36 + bm) bitmap[(size_t)s * bm + (o - 36)] = rec[o];
+}
+
+hipError_t launch_partition_pack(const uint8_t* d_root, const uint32_t* d_ntx, const uint8_t* d_bm, uint32_t n,
+                                 uint32_t per, uint32_t R, uint32_t bm, int32_t status, uint8_t* d_block,
+                                 hipStream_t st) {
+    uint32_t total = per * R;
+    hipLaunchKernelGGL(k_partition_pack, dim3((total + 255) / 256 + 1), dim3(256), 0, st, d_root, d_ntx, d_bm, n, per,
+                       R, bm, status, d_block);
+    return hipGetLastError();
+}
+
+hipError_t launch_partition_unpack(const uint8_t* d_all, uint32_t nranks, uint32_t n_total, uint32_t R, uint32_t bm,
+                                   size_t B, uint8_t* d_root, uint32_t* d_ntx, uint8_t* d_bm, int32_t* d_rank_status,
+                                   hipStream_t st) {
+    uint32_t total = std::max(n_total * R, nranks);
+    if (!total) return hipSuccess;
+    hipLaunchKernelGGL(k_partition_unpack, dim3((total + 255) / 256), dim3(256), 0, st, d_all, nranks, n_total, R, bm,
+                       B, d_root, d_ntx, d_bm, d_rank_status);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- launchers

@@ -375,6 +375,64 @@ def _notary_validate_partition(self, my_bodies, n_total: int, chain_id: int = 1,
     return roots, ntx, bitmap, senders, status
 
 
+def partition_block_bytes(n_total: int, nranks: int, max_txs: int = 8192) -> int:
+    """Bytes of one rank's record block (gsv.h gsv_partition_block_bytes)."""
+    return int(_lib.load().gsv_partition_block_bytes(n_total, nranks, max_txs))
+
+
+def _notary_partition_prepare(self, h_off, n_total: int, nranks: int, rank: int, chain_id: int = 1,
+                              signer_kind: int = _lib.SIGNER_EIP155, max_txs: int = 8192):
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    cbuf = np.frombuffer(_be(chain_id) + b"\0", np.uint8)
+    check(_lib.load().gsv_notary_partition_prepare(self._h, _ptr(h_off), n_total, int(nranks), int(rank), _ptr(cbuf),
+                                                   len(_be(chain_id)), int(signer_kind), int(max_txs)))
+
+
+def _notary_validate_partition_dev(self, bodies_t, h_off, n_total: int, roots_t, ntx_t, bitmap_t, senders_t=None,
+                                   status_t=None, rank_status_t=None, chain_id: int = 1,
+                                   signer_kind: int = _lib.SIGNER_EIP155, max_txs: int = 8192, stream=None,
+                                   prepare=True):
+    """gsv.h gsv_notary_validate_partition_dev: this rank's block (HBM, host offsets h_off) in; every
+    shard's record out in HBM (validation + pack + one ncclAllGather + unpack on `stream`)."""
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    if prepare:
+        n, r = self.comm_info()
+        _notary_partition_prepare(self, h_off, n_total, n, r, chain_id, signer_kind, max_txs)
+    cbuf = np.frombuffer(_be(chain_id) + b"\0", np.uint8)
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_notary_validate_partition_dev(
+        self._h, _tptr(bodies_t), _ptr(h_off), n_total, _ptr(cbuf), len(_be(chain_id)), int(signer_kind),
+        int(max_txs), _tptr(roots_t), _tptr(ntx_t), _tptr(bitmap_t), _tptr(senders_t), _tptr(status_t),
+        _tptr(rank_status_t), sp))
+
+
+def _notary_partition_pack_dev(self, bodies_t, h_off, n_total: int, nranks: int, rank: int, block_t,
+                               senders_t=None, status_t=None, chain_id: int = 1,
+                               signer_kind: int = _lib.SIGNER_EIP155, max_txs: int = 8192, stream=None, prepare=True):
+    """gsv.h gsv_notary_partition_pack_dev: validate rank `rank`'s block and write its record block."""
+    h_off = np.ascontiguousarray(h_off, np.uint64)
+    if prepare:
+        _notary_partition_prepare(self, h_off, n_total, nranks, rank, chain_id, signer_kind, max_txs)
+    cbuf = np.frombuffer(_be(chain_id) + b"\0", np.uint8)
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_notary_partition_pack_dev(
+        self._h, _tptr(bodies_t), _ptr(h_off), n_total, int(nranks), int(rank), _ptr(cbuf), len(_be(chain_id)),
+        int(signer_kind), int(max_txs), _tptr(block_t), _tptr(senders_t), _tptr(status_t), sp))
+
+
+def _notary_partition_unpack_dev(self, blocks_t, n_total: int, nranks: int, roots_t, ntx_t, bitmap_t,
+                                 rank_status_t=None, max_txs: int = 8192, stream=None):
+    """gsv.h gsv_notary_partition_unpack_dev: nranks gathered blocks (rank order) -> shard-order records."""
+    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    check(_lib.load().gsv_notary_partition_unpack_dev(self._h, _tptr(blocks_t), n_total, int(nranks), int(max_txs),
+                                                      _tptr(roots_t), _tptr(ntx_t), _tptr(bitmap_t),
+                                                      _tptr(rank_status_t), sp))
+
+
+Context.notary_partition_prepare = _notary_partition_prepare
+Context.notary_validate_partition_dev = _notary_validate_partition_dev
+Context.notary_partition_pack_dev = _notary_partition_pack_dev
+Context.notary_partition_unpack_dev = _notary_partition_unpack_dev
 Context.comm_init = _comm_init
 Context.comm_info = _comm_info
 Context.notary_validate_partition = _notary_validate_partition

@@ -114,6 +114,15 @@ SIGNATURES = [
     ("gsv_shard_range", ctypes.c_int, [_sz, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
     ("gsv_notary_validate_partition", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, ctypes.c_int, ctypes.c_uint32,
                                                      _vp, _vp, _vp, _vp, _vp]),
+    ("gsv_notary_partition_prepare", ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp, _sz,
+                                                    ctypes.c_int, ctypes.c_uint32]),
+    ("gsv_notary_validate_partition_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, ctypes.c_int, ctypes.c_uint32,
+                                                         _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("gsv_partition_block_bytes", _sz, [_sz, ctypes.c_int, ctypes.c_uint32]),
+    ("gsv_notary_partition_pack_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp, _sz,
+                                                     ctypes.c_int, ctypes.c_uint32, _vp, _vp, _vp, _vp]),
+    ("gsv_notary_partition_unpack_dev", ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int, ctypes.c_uint32, _vp, _vp, _vp,
+                                                       _vp, _vp]),
 ]
 
 _lib = None

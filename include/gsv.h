@@ -244,7 +244,9 @@ int gsv_notary_validate_shards_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const 
 /* ---- synthetic collations (bench / test data; configs[3]) ----
  * Bodies of shards shard0 .. shard0+n_shards-1 (txs_per_shard x 128 B each, contiguous): signed
  * EIP-155 txs (chain id 1) blob-serialized 4 chunks per tx; every 128th tx invalid by construction
- * (high-s / wrong chain id / r not an x-coordinate).  Optional expected status and sender per tx. */
+ * (high-s / wrong chain id / r not an x-coordinate / recid flipped).  Optional expected status and
+ * sender per tx; exp_sender holds the SIGNER's address, which a recid-flipped tx (status OK) does not
+ * recover to. */
 int gsv_notary_synth_dev(gsv_ctx *ctx, uint64_t seed, uint32_t shard0, size_t n_shards, uint32_t txs_per_shard,
                          uint8_t *d_bodies, uint8_t *d_exp_status, uint8_t *d_exp_sender, void *stream);
 
@@ -312,11 +314,45 @@ int gsv_shard_range(size_t n_shards, int nranks, int rank, size_t *first, size_t
  * all-gathers the fixed-size per-shard records over RCCL, so every rank returns the records of all
  * n_total_shards shards in shard order: root32_all[32 S], ntx_all[S], valid_bitmap_all[S ceil(max_txs/8)].
  * senders_out / status_out (optional) cover this rank's own shards only ([count][max_txs]).
- * Needs gsv_comm_init (a context without one behaves as N = 1). */
+ * Needs gsv_comm_init (a context without one behaves as N = 1).
+ * Collective contract (as for RCCL itself): every rank calls it with the same n_total_shards, chain id,
+ * signer and max_txs.  An error in those returns on every rank before the collective.  A failure local
+ * to one rank (its bodies, a body > 2^20 bytes, device memory, a HIP error) does NOT skip the
+ * collective: the rank all-gathers an empty block carrying its status, and EVERY rank returns the
+ * status of the lowest failing rank (the records of the failing ranks' shards are zero). */
 int gsv_notary_validate_partition(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off, size_t n_total_shards,
                                   const uint8_t *chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
                                   uint8_t *root32_all, uint32_t *ntx_all, uint8_t *valid_bitmap_all,
                                   uint8_t *senders_out, uint8_t *status_out);
+/* Device-resident form (the one bench.py times at N > 1): d_bodies holds this rank's block in HBM at the
+ * host offsets h_off (count + 1 entries, count from gsv_shard_range); outputs in HBM; enqueues the block's
+ * validation, the record pack, one ncclAllGather and the unpack on `stream` and returns.
+ * d_rank_status (optional, int32 [nranks]) receives every rank's local status (nonzero: that rank's
+ * shards have zero records).  A rank-local failure joins the collective as above and returns its code
+ * (the other ranks see it in d_rank_status).  gsv_notary_partition_prepare prepares it for exactly
+ * (h_off, n_total_shards, nranks, rank, chain id, signer, max_txs); the context's communicator gives
+ * nranks / rank. */
+int gsv_notary_partition_prepare(gsv_ctx *ctx, const uint64_t *h_off, size_t n_total_shards, int nranks, int rank,
+                                 const uint8_t *chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs);
+int gsv_notary_validate_partition_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off,
+                                      size_t n_total_shards, const uint8_t *chain_id, size_t chain_id_len,
+                                      int signer_kind, uint32_t max_txs, uint8_t *d_root32_all, uint32_t *d_ntx_all,
+                                      uint8_t *d_valid_bitmap_all, uint8_t *d_senders, uint8_t *d_status,
+                                      int32_t *d_rank_status, void *stream);
+/* The same two halves for a caller with its own transport (e.g. records gathered across nodes, one
+ * shard per node as the reference runs): pack validates rank `rank`'s block and writes its record block
+ * (gsv_partition_block_bytes: header {int32 status, uint32 shards} + ceil(S/N) records of
+ * root 32 | ntx 4 | bitmap, padded to 8) into d_block; unpack takes the nranks blocks in rank order and
+ * writes the per-shard outputs in shard order (+ d_rank_status).  pack needs
+ * gsv_notary_partition_prepare with the same (nranks, rank). */
+size_t gsv_partition_block_bytes(size_t n_total_shards, int nranks, uint32_t max_txs);
+int gsv_notary_partition_pack_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off, size_t n_total_shards,
+                                  int nranks, int rank, const uint8_t *chain_id, size_t chain_id_len, int signer_kind,
+                                  uint32_t max_txs, uint8_t *d_block, uint8_t *d_senders, uint8_t *d_status,
+                                  void *stream);
+int gsv_notary_partition_unpack_dev(gsv_ctx *ctx, const uint8_t *d_blocks, size_t n_total_shards, int nranks,
+                                    uint32_t max_txs, uint8_t *d_root32_all, uint32_t *d_ntx_all,
+                                    uint8_t *d_valid_bitmap_all, int32_t *d_rank_status, void *stream);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,8 @@ code in oracle/_ref and the pinned restatement):
     configs[0]  types.Sender over the 10,000 EIP-155 txs       -> SHA-256 of the senders
     configs[1]  the bench's 2^20 signatures (seed 1000)         -> SHA-256 of the recovered addresses
     configs[2]  100 x 1 MiB xoshiro256** bodies                 -> all 100 chunk roots
+    configs[3]  the bench's 100 shards x 8,192 txs (seed 777)     -> 100 chunk roots + digests of the
+                bodies, validity bitmaps, senders and statuses (recid-flip rows: sender != signer)
     configs[4]  the bench's first 1,024 4-pair checks (seed 5000) -> their verdicts
 """
 import hashlib
@@ -86,3 +88,43 @@ def test_configs0_sender(ctx, oracle):
     addr, st = ctx.tx_sender_batch(txs, g["chain_id"], 0)
     assert (st == 0).all()
     assert hashlib.sha256(addr.tobytes()).hexdigest() == g["senders_sha256"]
+
+
+def test_configs3_hundred_shards_full_size(ctx):
+    """configs[3] at its own size on one GPU: the GPU generator's 100 x 8,192-tx bodies equal the
+    reference signer's byte for byte, and notary validation of all 819,200 txs (blob decode, RLP,
+    Sender, chunk root) equals the CPU validation (sharding/collation.go:193-206,
+    sharding/utils/marshal.go:144-198, sharding/notary/notary.go:413-445)."""
+    import hashlib
+    import torch
+    g = golden("configs.json")["configs3_notary"]
+    nsh, txs = g["shards"], g["txs_per_shard"]
+    dev = torch.device("cuda", ctx.device)
+    bodies = torch.empty((nsh * txs * 128,), dtype=torch.uint8, device=dev)
+    exp_st = torch.empty((nsh * txs,), dtype=torch.uint8, device=dev)
+    exp_snd = torch.empty((nsh * txs, 20), dtype=torch.uint8, device=dev)
+    ctx.notary_synth_dev(g["seed"], 0, nsh, txs, bodies, exp_st, exp_snd)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(bodies.cpu().numpy().tobytes()).hexdigest() == g["bodies_sha256"]
+    off = np.arange(nsh + 1, dtype=np.uint64) * txs * 128
+    root = torch.empty((nsh, 32), dtype=torch.uint8, device=dev)
+    ntx = torch.empty((nsh,), dtype=torch.int32, device=dev)
+    bm = torch.empty((nsh, txs // 8), dtype=torch.uint8, device=dev)
+    snd = torch.empty((nsh, txs, 20), dtype=torch.uint8, device=dev)
+    st = torch.empty((nsh, txs), dtype=torch.uint8, device=dev)
+    ctx.notary_validate_shards_dev(bodies, off, root, ntx, bm, snd, st, max_txs=txs)
+    torch.cuda.synchronize()
+    assert (ntx.cpu().numpy() == txs).all()
+    assert [bytes(r).hex() for r in root.cpu().numpy()] == g["roots"]
+    assert hashlib.sha256(bm.cpu().numpy().tobytes()).hexdigest() == g["bitmaps_sha256"]
+    assert hashlib.sha256(st.cpu().numpy().tobytes()).hexdigest() == g["status_sha256"]
+    assert hashlib.sha256(snd.cpu().numpy().tobytes()).hexdigest() == g["senders_sha256"]
+    # the recid-flip class: status OK, the generator's expectation, but the sender is not the signer
+    assert torch.equal(st.view(-1), exp_st)
+    j = torch.arange(txs, device=dev)
+    flip = ((j % 128 == 127) & ((j // 128) % 4 == 3)).repeat(nsh)
+    same = (snd.view(-1, 20) == exp_snd).all(dim=1)
+    assert bool(same[~flip & (exp_st == 0)].all()) and not bool(same[flip].any())
+    for row in g["recid_flip_shard0"]:
+        assert bytes(snd[0, row["tx"]].cpu().numpy()).hex() == row["sender"]
+        assert bytes(exp_snd[row["tx"]].cpu().numpy()).hex() == row["signer"]

@@ -93,8 +93,14 @@ def test_notary_synthetic_shards(ctx, oracle):
     roots, ntx, bitmap, senders, status = _check(ctx, oracle, bodies, 1, 0, per)
     es = exp_st.cpu().numpy().reshape(n_sh, per)
     assert (status == es).all()
-    assert (senders == exp_snd.cpu().numpy().reshape(n_sh, per, 20)).all()
-    assert (es == ST_OK).sum() == n_sh * per - n_sh * (per // 128)
+    # generator classes (gi / 128) % 4 with gi = shard * per + j: class 3 flips the recid, a valid
+    # signature of another key (status OK, sender != the signer the generator expects)
+    gi = (np.arange(7, 7 + n_sh)[:, None] * per + np.arange(per)[None, :])
+    flip = (gi % 128 == 127) & ((gi // 128) % 4 == 3)
+    assert flip.any()
+    same = (senders == exp_snd.cpu().numpy().reshape(n_sh, per, 20)).all(axis=2)
+    assert same[~flip].all() and not same[flip].any()
+    assert (es == ST_OK).sum() == n_sh * per - n_sh * (per // 128) + flip.sum()
     # the device-resident entry point gives the same records
     h_off = np.arange(n_sh + 1, dtype=np.uint64) * per * 128
     r_t = torch.empty((n_sh, 32), dtype=torch.uint8, device="cuda")

@@ -1,8 +1,13 @@
-"""The native shard partition + RCCL all-gather entry point (gsv.h gsv_notary_validate_partition,
-SURVEY.md §8e; reference partition sharding/node/backend.go:245-284): on one GPU as a one-rank RCCL
-communicator, every shard's gathered record equals gsv_notary_validate_shards' on the same bodies.
-(More RCCL ranks need more GPUs: the driver's 8-GPU bench runs the partition through torch.distributed;
-the record layout and block arithmetic are shared with gsv/shards.py and tested with gloo.)"""
+"""The native shard partition + RCCL all-gather entry points (gsv.h gsv_notary_validate_partition[_dev],
+gsv_notary_partition_pack_dev / _unpack_dev; reference partition
+sharding/node/backend.go:245-284).
+
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so on the one-GPU box:
+  * the RCCL entry points run as a one-rank communicator against gsv_notary_validate_shards, including
+    the rank-local failure path (the rank still reaches the collective and reports its status);
+  * 2 and 3 rank processes run the same pack -> all-gather -> unpack through the C ABI with the
+    all-gather over gloo (host): the block layout and the unpack offsets of ranks q > 0 are the ones the
+    RCCL path uses (bench.py --gpus N runs gsv_notary_validate_partition_dev over RCCL)."""
 import numpy as np
 import pytest
 
@@ -32,12 +37,54 @@ def test_partition_one_rank_equals_local_validation(ctx):
     # a rank with an empty block still receives every shard's record (here: 0 shards of 0)
     r = ctx.notary_validate_partition([], 0, max_txs=txs)
     assert r[0].shape == (0, 32)
+    # device-resident form on the same communicator
+    off = np.arange(nsh + 1, dtype=np.uint64) * txs * 128
+    root = torch.zeros((nsh, 32), dtype=torch.uint8, device=dev)
+    ntx = torch.zeros((nsh,), dtype=torch.int32, device=dev)
+    bm = torch.zeros((nsh, txs // 8), dtype=torch.uint8, device=dev)
+    rst = torch.full((1,), -99, dtype=torch.int32, device=dev)
+    ctx.notary_validate_partition_dev(bodies_t, off, nsh, root, ntx, bm, rank_status_t=rst, max_txs=txs)
+    torch.cuda.synchronize()
+    assert np.array_equal(root.cpu().numpy(), want[0]) and np.array_equal(bm.cpu().numpy(), want[2])
+    assert (ntx.cpu().numpy() == txs).all() and int(rst[0]) == 0
+
+
+def test_partition_local_failure_still_joins_the_collective(ctx):
+    """a rank-local failure returns its status after the all-gather, not before it."""
+    import torch
+    from gsv._lib import GsvError, E_TOO_LARGE, E_NOT_PREPARED
+    txs = 256
+    dev = torch.device("cuda", ctx.device)
+    ctx.comm_init(gsv.comm_unique_id(), 1, 0)
+    # host form: a body over 2^20 bytes (sharding/collation.go:45)
+    with pytest.raises(GsvError) as e:
+        ctx.notary_validate_partition([bytes((1 << 20) + 1)], 1, max_txs=txs)
+    assert e.value.code == E_TOO_LARGE
+    # device form, never prepared for these offsets: the rank status says why
+    off = np.array([0, txs * 128], np.uint64)
+    nb = torch.zeros(txs * 128, dtype=torch.uint8, device=dev)
+    root = torch.full((1, 32), 7, dtype=torch.uint8, device=dev)
+    ntx = torch.zeros((1,), dtype=torch.int32, device=dev)
+    bm = torch.zeros((1, txs // 8), dtype=torch.uint8, device=dev)
+    rst = torch.zeros((1,), dtype=torch.int32, device=dev)
+    with pytest.raises(GsvError) as e:
+        ctx.notary_validate_partition_dev(nb, off + 16, 1, root, ntx, bm, rank_status_t=rst, max_txs=txs,
+                                          prepare=False)
+    assert e.value.code == E_NOT_PREPARED
+    torch.cuda.synchronize()
+    assert int(rst[0]) == E_NOT_PREPARED and int(root.sum()) == 0 and int(ntx[0]) == 0
+    # and the context still works afterwards
+    ctx.notary_validate_partition_dev(nb, off, 1, root, ntx, bm, rank_status_t=rst, max_txs=txs)
+    torch.cuda.synchronize()
+    assert int(rst[0]) == 0 and int(ntx[0]) == 0  # an all-zero body holds no blobs
 
 
 def _rank_worker(rank, world, port, nsh, txs, q):
-    """one rank process: validate this rank's shard block on the GPU, pack its records on the GPU,
-    all-gather them over gloo (the collective bench.py runs over RCCL), check every shard's record
-    against a whole-batch validation in this process"""
+    """one rank process: validate this rank's shard block and pack its record block through the C ABI
+    (gsv_notary_partition_pack_dev), all-gather the blocks over gloo (the step RCCL does in
+    gsv_notary_validate_partition_dev), unpack them through the C ABI (gsv_notary_partition_unpack_dev),
+    and check every shard's record against a whole-batch validation in this process; the torch form
+    of the same records (gsv/shards.py) must agree."""
     import os
     import torch
     import torch.distributed as dist
@@ -65,7 +112,24 @@ def _rank_worker(rank, world, port, nsh, txs, q):
         rec = torch.zeros((per, SH.record_bytes(txs)), dtype=torch.uint8, device=dev)
         SH.pack_records(rec, root, cnt, bm)
         g = SH.gather_records(rec.cpu(), world)  # gloo: host tensors
-        g_root, g_ntx, g_bm = SH.unpack_records(g, world, nsh, txs)
+        t_root, t_ntx, t_bm = SH.unpack_records(g, world, nsh, txs)
+        # the C-ABI form: pack -> all-gather (gloo here, RCCL in the combined entry point) -> unpack
+        B = G.partition_block_bytes(nsh, world, txs)
+        blk = torch.zeros((B,), dtype=torch.uint8, device=dev)
+        ctx.notary_partition_pack_dev(nb, off, nsh, world, rank, blk, max_txs=txs)
+        torch.cuda.synchronize()
+        parts = [torch.empty((B,), dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, blk.cpu())
+        allb_t = torch.cat(parts).to(dev)
+        g_root = torch.zeros((nsh, 32), dtype=torch.uint8, device=dev)
+        g_ntx = torch.zeros((nsh,), dtype=torch.int32, device=dev)
+        g_bm = torch.zeros((nsh, txs // 8), dtype=torch.uint8, device=dev)
+        g_rst = torch.full((world,), -1, dtype=torch.int32, device=dev)
+        ctx.notary_partition_unpack_dev(allb_t, nsh, world, g_root, g_ntx, g_bm, g_rst, max_txs=txs)
+        torch.cuda.synchronize()
+        g_root, g_ntx, g_bm = g_root.cpu(), g_ntx.cpu(), g_bm.cpu()
+        assert (g_rst.cpu() == 0).all()
+        assert torch.equal(g_root, t_root) and torch.equal(g_ntx, t_ntx) and torch.equal(g_bm, t_bm)
         # the whole batch validated in this process
         allb = torch.empty((nsh * txs * 128,), dtype=torch.uint8, device=dev)
         ctx.notary_synth_dev(4242, 0, nsh, txs, allb)
