@@ -456,6 +456,7 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     a_bm = torch.zeros((N_SHARDS, NOTARY_TXS // 8), dtype=torch.uint8, device=dev)
     a_rst = torch.full((ws,), -1, dtype=torch.int32, device=dev)
     n_st = torch.empty((max(nloc, 1), NOTARY_TXS), dtype=torch.uint8, device=dev)
+    stream.wait_stream(torch.cuda.current_stream())  # the fills above ran on torch's stream
     ctx.notary_partition_prepare(n_off, N_SHARDS, ws, rank, max_txs=NOTARY_TXS)
 
     def notary_step(with_status=False):
@@ -484,6 +485,7 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     t_root = torch.zeros((max(nloc, 1), 32), dtype=torch.uint8, device=dev)
     t_cnt = torch.zeros((max(nloc, 1),), dtype=torch.int32, device=dev)
     t_bm = torch.zeros((max(nloc, 1), NOTARY_TXS // 8), dtype=torch.uint8, device=dev)
+    stream.wait_stream(torch.cuda.current_stream())
     if nloc:
         ctx.notary_validate_shards_dev(nb, n_off, t_root, t_cnt, t_bm, None, None, max_txs=NOTARY_TXS,
                                        stream=stream)

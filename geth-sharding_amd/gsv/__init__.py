@@ -158,7 +158,7 @@ class Context:
     def ecrecover_batch_dev(self, msg_t, sig_t, pub_t, addr_t, st_t, stream=None):
         """torch uint8 CUDA tensors already in HBM; enqueues on `stream` (torch stream or None)."""
         n = msg_t.shape[0]
-        sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        sp = _sp(stream)
         check(_lib.load().gsv_ecrecover_batch_dev(
             self._h, ctypes.c_void_p(msg_t.data_ptr()), ctypes.c_void_p(sig_t.data_ptr()), n,
             ctypes.c_void_p(pub_t.data_ptr()) if pub_t is not None else None,
@@ -167,7 +167,7 @@ class Context:
 
     def synth_sign_dev(self, seed, msg_t, sig_t, pub_t=None, addr_t=None, stream=None):
         n = msg_t.shape[0]
-        sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        sp = _sp(stream)
         check(_lib.load().gsv_synth_sign_dev(
             self._h, ctypes.c_uint64(seed), n, ctypes.c_void_p(msg_t.data_ptr()),
             ctypes.c_void_p(sig_t.data_ptr()),
@@ -176,7 +176,7 @@ class Context:
 
     def keccak256_batch_dev(self, data_t, off_t, out_t, stream=None):
         n = out_t.shape[0]
-        sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        sp = _sp(stream)
         check(_lib.load().gsv_keccak256_batch_dev(self._h, ctypes.c_void_p(data_t.data_ptr()),
                                                   ctypes.c_void_p(off_t.data_ptr()), n,
                                                   ctypes.c_void_p(out_t.data_ptr()), sp))
@@ -229,7 +229,7 @@ def _chunk_root_batch_dev(self, bodies_t, h_off, roots_t, stream=None, prepare=T
     n = h_off.shape[0] - 1
     if prepare:
         _chunk_root_prepare(self, h_off)
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_chunk_root_batch_dev(self._h, ctypes.c_void_p(bodies_t.data_ptr()), _ptr(h_off), n,
                                                ctypes.c_void_p(roots_t.data_ptr()), sp))
 
@@ -257,7 +257,7 @@ def _pairing_check_batch_dev(self, in_t, h_off, verdict_t, stream=None, prepare=
     n = h_off.shape[0] - 1
     if prepare:
         _pairing_prepare(self, h_off)
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_bn256_pairing_check_batch_dev(self._h, ctypes.c_void_p(in_t.data_ptr()), _ptr(h_off),
                                                         n, ctypes.c_void_p(verdict_t.data_ptr()), sp))
 
@@ -265,10 +265,23 @@ def _pairing_check_batch_dev(self, in_t, h_off, verdict_t, stream=None, prepare=
 def _bn256_synth_checks_dev(self, seed, out_t, expect_t=None, stream=None):
     """configs[4] synthetic 4-pair checks into out_t (torch uint8 CUDA, nchecks x 768)."""
     n = out_t.shape[0]
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_bn256_synth_checks_dev(
         self._h, ctypes.c_uint64(seed), n, ctypes.c_void_p(out_t.data_ptr()),
         ctypes.c_void_p(expect_t.data_ptr()) if expect_t is not None else None, sp))
+
+
+def _sp(stream):
+    """HIP stream handle for a *_dev call: None = the context's own stream.  torch's default (null)
+    stream has handle 0, which the C ABI reads as "the context stream" — refused here, because the call
+    would then run unordered with the caller's work on that stream."""
+    if stream is None:
+        return None
+    h = int(stream.cuda_stream)
+    if h == 0:
+        raise ValueError("gsv: pass a non-default torch.cuda.Stream (or None for the context stream); "
+                         "the null stream's handle 0 means the context stream in the C ABI")
+    return ctypes.c_void_p(h)
 
 
 def _tptr(t):
@@ -315,7 +328,7 @@ def _notary_validate_shards_dev(self, bodies_t, h_off, roots_t, ntx_t, bitmap_t,
         _notary_prepare(self, h_off, chain_id, signer_kind, max_txs)
     cid = _be(chain_id)
     cbuf = np.frombuffer(cid + b"\0", np.uint8)
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_notary_validate_shards_dev(self._h, _tptr(bodies_t), _ptr(h_off), n, _ptr(cbuf), len(cid),
                                                      int(signer_kind), int(max_txs), _tptr(roots_t), _tptr(ntx_t),
                                                      _tptr(bitmap_t), _tptr(senders_t), _tptr(status_t), sp))
@@ -323,7 +336,7 @@ def _notary_validate_shards_dev(self, bodies_t, h_off, roots_t, ntx_t, bitmap_t,
 
 def _notary_synth_dev(self, seed, shard0, n_shards, txs_per_shard, bodies_t, exp_status_t=None, exp_sender_t=None,
                       stream=None):
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_notary_synth_dev(self._h, ctypes.c_uint64(seed), int(shard0), int(n_shards),
                                            int(txs_per_shard), _tptr(bodies_t), _tptr(exp_status_t),
                                            _tptr(exp_sender_t), sp))
@@ -399,7 +412,7 @@ def _notary_validate_partition_dev(self, bodies_t, h_off, n_total: int, roots_t,
         n, r = self.comm_info()
         _notary_partition_prepare(self, h_off, n_total, n, r, chain_id, signer_kind, max_txs)
     cbuf = np.frombuffer(_be(chain_id) + b"\0", np.uint8)
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_notary_validate_partition_dev(
         self._h, _tptr(bodies_t), _ptr(h_off), n_total, _ptr(cbuf), len(_be(chain_id)), int(signer_kind),
         int(max_txs), _tptr(roots_t), _tptr(ntx_t), _tptr(bitmap_t), _tptr(senders_t), _tptr(status_t),
@@ -414,7 +427,7 @@ def _notary_partition_pack_dev(self, bodies_t, h_off, n_total: int, nranks: int,
     if prepare:
         _notary_partition_prepare(self, h_off, n_total, nranks, rank, chain_id, signer_kind, max_txs)
     cbuf = np.frombuffer(_be(chain_id) + b"\0", np.uint8)
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_notary_partition_pack_dev(
         self._h, _tptr(bodies_t), _ptr(h_off), n_total, int(nranks), int(rank), _ptr(cbuf), len(_be(chain_id)),
         int(signer_kind), int(max_txs), _tptr(block_t), _tptr(senders_t), _tptr(status_t), sp))
@@ -423,7 +436,7 @@ def _notary_partition_pack_dev(self, bodies_t, h_off, n_total: int, nranks: int,
 def _notary_partition_unpack_dev(self, blocks_t, n_total: int, nranks: int, roots_t, ntx_t, bitmap_t,
                                  rank_status_t=None, max_txs: int = 8192, stream=None):
     """gsv.h gsv_notary_partition_unpack_dev: nranks gathered blocks (rank order) -> shard-order records."""
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_notary_partition_unpack_dev(self._h, _tptr(blocks_t), n_total, int(nranks), int(max_txs),
                                                       _tptr(roots_t), _tptr(ntx_t), _tptr(bitmap_t),
                                                       _tptr(rank_status_t), sp))
@@ -477,7 +490,7 @@ def _derive_sha_batch_dev(self, vals_t, voff, list_off, roots_t, stream=None, pr
     n = list_off.shape[0] - 1
     if prepare:
         _derive_sha_prepare(self, voff, list_off)
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_derive_sha_batch_dev(self._h, _tptr(vals_t), _ptr(voff), _ptr(list_off), n,
                                                _tptr(roots_t), sp))
 
@@ -506,7 +519,7 @@ def _collation_poc_batch_dev(self, bodies_t, h_off, salt: bytes, out_t, stream=N
     if prepare:
         _collation_poc_prepare(self, h_off, salt)
     sb = np.frombuffer(bytes(salt) + b"\0", np.uint8)
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_collation_poc_batch_dev(self._h, _tptr(bodies_t), _ptr(h_off), n, _ptr(sb), len(salt),
                                                   _tptr(out_t), sp))
 
@@ -537,7 +550,7 @@ def _collation_header_verify_batch_dev(self, sid_t, root_t, per_t, prop_t, sig_t
     n = sid_t.shape[0]
     if prepare:
         check(_lib.load().gsv_collation_header_prepare(self._h, n))
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_collation_header_verify_batch_dev(self._h, _tptr(sid_t), _tptr(root_t), _tptr(per_t),
                                                             _tptr(prop_t), _tptr(sig_t), _tptr(nil_t), n,
                                                             _tptr(hash_t), _tptr(signer_t), _tptr(st_t), sp))
@@ -569,7 +582,7 @@ def _ecrecover_precompile_batch(self, inputs):
 def _ecrecover_precompile_batch_dev(self, in_t, out_t, ok_t, stream=None):
     """in_t: torch uint8 CUDA tensor (n, 128) of right-padded precompile inputs."""
     n = in_t.shape[0]
-    sp = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    sp = _sp(stream)
     check(_lib.load().gsv_ecrecover_precompile_batch_dev(self._h, _tptr(in_t), n, _tptr(out_t), _tptr(ok_t), sp))
 
 

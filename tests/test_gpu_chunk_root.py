@@ -58,14 +58,17 @@ def test_chunk_root_large_lengths(ctx):
     # h_off holds consecutive start/end pairs only when bodies are contiguous: pass exact ends via
     # one call per length class instead (a batch of equal-length bodies shares one plan)
     roots = torch.empty((len(bodies), 32), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
     for n in sorted({len(b) for b in bodies}):
         idx = [i for i, b in enumerate(bodies) if len(b) == n]
-        sub = torch.cat([d[int(starts[i]):int(starts[i]) + n] for i in idx])
-        h_off = np.arange(len(idx) + 1, dtype=np.uint64) * n
-        r = torch.empty((len(idx), 32), dtype=torch.uint8, device="cuda")
-        ctx.chunk_root_batch_dev(sub, h_off, r)
-        for k, i in enumerate(idx):
-            roots[i] = r[k]
+        with torch.cuda.stream(st):
+            sub = torch.cat([d[int(starts[i]):int(starts[i]) + n] for i in idx])
+            h_off = np.arange(len(idx) + 1, dtype=np.uint64) * n
+            r = torch.empty((len(idx), 32), dtype=torch.uint8, device="cuda")
+            ctx.chunk_root_batch_dev(sub, h_off, r, stream=st)
+            for k, i in enumerate(idx):
+                roots[i] = r[k]
     torch.cuda.synchronize()
     got = [bytes(x).hex() for x in roots.cpu().numpy()]
     assert got == [c["root"] for c in g]

@@ -121,6 +121,7 @@ def _rank_worker(rank, world, port, nsh, txs, q):
         parts = [torch.empty((B,), dtype=torch.uint8) for _ in range(world)]
         dist.all_gather(parts, blk.cpu())
         allb_t = torch.cat(parts).to(dev)
+        torch.cuda.synchronize()  # the unpack runs on the context's stream
         g_root = torch.zeros((nsh, 32), dtype=torch.uint8, device=dev)
         g_ntx = torch.zeros((nsh,), dtype=torch.int32, device=dev)
         g_bm = torch.zeros((nsh, txs // 8), dtype=torch.uint8, device=dev)

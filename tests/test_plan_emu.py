@@ -1,0 +1,59 @@
+"""CPU check of the chunk-root trie PLAN (the product's host code, gsv::build_trie_plan in libgsv.so):
+tests/native/plan_emu.cpp encodes every node the plan lists the way the kernels do and the root must
+equal the oracle restatement's DeriveSha (core/types/derive_sha.go:32-41, trie/hasher.go:153-165) for
+every tested length, including the large lengths of the committed fixtures (tests/golden/chunk_root.json
+large_cases).  No GPU: a mismatch here is a plan bug, a GPU-only mismatch a kernel bug."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+
+LIBDIR = os.path.join(ROOT, "geth-sharding_amd", "gsv")
+
+
+@pytest.fixture(scope="module")
+def emu(tmp_path_factory, oracle):
+    if not os.path.exists(os.path.join(LIBDIR, "libgsv.so")):
+        pytest.skip("libgsv.so not built")
+    out = tmp_path_factory.mktemp("planemu") / "plan_emu.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", str(out),
+                    os.path.join(ROOT, "tests", "native", "plan_emu.cpp"),
+                    "-L" + LIBDIR, "-lgsv", "-Wl,-rpath," + LIBDIR,
+                    "-L" + os.path.join(ROOT, "oracle"), "-l:liboracle.so", "-Wl,-rpath," + os.path.join(ROOT, "oracle")],
+                   check=True)
+    L = ctypes.CDLL(str(out))
+    L.plan_emu_root.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int),
+                                ctypes.POINTER(ctypes.c_int)]
+    return L
+
+
+def _root(emu, body):
+    out = ctypes.create_string_buffer(32)
+    h, t = ctypes.c_int(), ctypes.c_int()
+    assert emu.plan_emu_root(bytes(body) + b"\0", len(body), out, ctypes.byref(h), ctypes.byref(t)) == 0
+    return out.raw, h.value, t.value
+
+
+@pytest.mark.parametrize("ns", [list(range(1, 300)), [4095, 4096, 4097, 65535, 65536, 65537, 70000, 70001, 70002],
+                                [69631, 69632, 69633, 69888, 69904, 69905, 70016, 70017, 71000, 100000]])
+def test_plan_matches_oracle(emu, oracle, ns):
+    rng = np.random.default_rng(len(ns))
+    for n in ns:
+        body = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        r, _, _ = _root(emu, body)
+        assert r == oracle.derive_sha_bytes(body), n
+
+
+def test_plan_large_fixture_lengths(emu):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import xoshiro_bytes
+    fill = {"zero": 0, "7f": 0x7F, "80": 0x80, "ff": 0xFF}
+    for c in golden("chunk_root.json")["large_cases"]:
+        body = xoshiro_bytes(c["xoshiro_seed"], c["n"]) if c["fill"] == "random" else bytes([fill[c["fill"]]]) * c["n"]
+        r, _, _ = _root(emu, body)
+        assert r.hex() == c["root"], (c["n"], c["fill"])
