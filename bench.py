@@ -63,7 +63,8 @@ VALU_ISSUE_PEAK = 0.5
 PEAK_LANE_OPS = SIMDS * 64 * VALU_ISSUE_PEAK * CLOCK          # 7.86e13 full-rate 32-bit lane-ops/s
 PEAK_MAC = SIMDS * 16 * CLOCK                                 # 3.93e13 v_mad_u64_u32 lane-ops/s
 HBM_PEAK_GBPS = 8000.0
-PROFILES = os.path.join(ROOT, "profiles", "r02")
+ROUND = "r03"
+PROFILES = os.path.join(ROOT, "profiles", ROUND)
 LEGS = ["ecrecover", "chunk_root", "notary", "keccak", "tx_root", "poc", "headers", "pairing"]
 
 
@@ -105,7 +106,7 @@ def int_lane_ops(k, ms):
     ops = (k["sq_insts_valu_int32"] + k.get("sq_insts_valu_int64", 0.0)) * 64
     return {"per_launch": ops, "achieved_per_s": round(ops / (ms * 1e-3), 1), "peak_per_s": PEAK_LANE_OPS,
             "frac": round(ops / (ms * 1e-3) / PEAK_LANE_OPS, 4),
-            "source": "SQ_INSTS_VALU_INT32 + SQ_INSTS_VALU_INT64 (profiles/r02/pmc_*.json)"}
+            "source": f"SQ_INSTS_VALU_INT32 + SQ_INSTS_VALU_INT64 (profiles/{ROUND}/pmc_*.json)"}
 
 
 # ----------------------------------------------------------------------------- ranks
@@ -170,8 +171,23 @@ def host_info():
                     break
     except OSError:
         pass
-    # the box gives one GPU a 16-CPU share of the host (os.cpu_count() shows the whole machine)
-    return {"nproc": os.cpu_count(), "cpu_model": model, "threads_all_core": min(16, os.cpu_count() or 1)}
+    # all_core runs one host thread per CPU of ONE GPU's share of the node: nproc / 8 on an 8-GPU node
+    # (32 of the EPYC box's 256 threads).  The box's cgroup may cap the CPU time below that
+    # (cpu.max); the quota is reported beside the thread count so the figure reads right.
+    nproc = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = nproc
+    return {"nproc": nproc, "cpu_model": model, "threads_all_core": max(1, nproc // 8), "affinity": affinity,
+            "cgroup_cpu_quota": quota}
 
 
 # ----------------------------------------------------------------------------- dry run (CPU, gloo)
@@ -320,7 +336,7 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
     k_ms, k_n = ctx.kernel_time(_lib.K_ECRECOVER)
     k_avg_ms = max_over_ranks(k_ms / max(k_n, 1), ws)
     rate = ws * N_SIGS * args.steps / dt
-    k = pmc("gsv::k_ecrecover")
+    k = pmc("gsv::k_ecrecover", "pmc_ecrecover.json")
     ref_ach = MACS_PER_RECOVERY_REF * N_SIGS / (k_avg_ms * 1e-3)
     oc = opcount("recovery")
     act = oc["mac_equiv"] * N_SIGS / (k_avg_ms * 1e-3) if oc else None
@@ -329,7 +345,9 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
             "frac_actual": round(act / PEAK_MAC, 4) if act else None,
             "mac_equiv_per_recovery_reference": MACS_PER_RECOVERY_REF,
             "mac_equiv_per_recovery_actual": oc["mac_equiv"] if oc else None,
-            "traffic": pmc_traffic(k), "traffic_source": "profiles/r02/pmc_all.json" if pmc_traffic(k) else None,
+            "traffic": pmc_traffic(k),
+            "traffic_source": f"profiles/{ROUND}/pmc_ecrecover.json" if pmc_traffic(k) else None,
+            "profiled_kernel_avg_ms": k.get("avg_ms"),
             "algorithmic_bytes_per_launch": N_SIGS * (32 + 65 + 65 + 20 + 1),
             # by design: one 80-byte affine comb entry per 20-bit window of u1 (13 per recovery) from the
             # 1.09 GB table in HBM (gsv_internal.h GSV_COMB_BITS)
@@ -341,7 +359,7 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
                                     f"{MACS_PER_RECOVERY_REF} per recovery for the reference algorithm "
                                     "(libsecp256k1 Strauss-wNAF), mac_equiv_per_recovery_actual = the "
                                     "v_mad_u64_u32 our kernel executes per recovery (9x29-bit fe9 products 100, "
-                                    "squarings 64; GLV w=4 + comb; instrumented build, profiles/r02/opcount.json)"}
+                                    "squarings 64; GLV w=4 + comb; instrumented build, profiles/{ROUND}/opcount.json)".format(ROUND=ROUND)}
     state = {"msg": msg, "sig": sig, "epub": epub}
     return {"rate": rate, "dt": dt, "roofline": roof}, state
 
@@ -402,10 +420,11 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
             "frac": round(bot_ach / ceiling, 4) if ceiling else None,
             "peak_basis": f"instruction floor: {VALU_ISSUE_PEAK} wave64 VALU instructions per SIMD-cycle x 1024 "
                           "SIMDs x 2.4 GHz x 64 lanes / VALU instructions per permutation (PMC SQ_INSTS_VALU of a "
-                          "chunk-root-only pass, profiles/r02/pmc_chunk_root.json)",
+                          f"chunk-root-only pass, profiles/{ROUND}/pmc_chunk_root.json)",
             "valu_instr_per_permutation": round(ipp, 1) if ipp else None,
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
-            "traffic": traffic, "algorithmic_bytes_per_launch": N_SHARDS * BODY,
+            # the body bytes read + every bottom node's raw 32-byte hash written into its parent's slot
+            "traffic": traffic, "algorithmic_bytes_per_launch": N_SHARDS * BODY + bot_perms * 32,
             "hbm_GBps": round(traffic / (k["avg_ms"] * 1e-3) / 1e9, 1) if traffic and k.get("avg_ms") else None,
             "hbm_frac": round(traffic / (k["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
             if traffic and k.get("avg_ms") else None,
@@ -583,7 +602,7 @@ def leg_keccak(ctx, stream, dev, ws, rank, args):
             "achieved": round(ach / 1e9, 3), "peak": round(ceiling / 1e9, 3) if ceiling else None,
             "frac": round(ach / ceiling, 4) if ceiling else None,
             "peak_basis": "instruction floor (as chunk_root.roofline; PMC of a keccak-only pass, "
-                          "profiles/r02/pmc_keccak.json)",
+                          f"profiles/{ROUND}/pmc_keccak.json)",
             "valu_instr_per_permutation": round(ipp, 1) if ipp else None,
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
             "traffic": traffic, "algorithmic_bytes_per_launch": int(voff[-1]) + (nblk * ntx + 1) * 8 + nblk * ntx * 32,
@@ -725,10 +744,14 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     ref_ach = FP_MULS_PER_CHECK_REF * MACS_PER_FP_MUL * nloc / (k_tot * 1e-3)
     oc = opcount("pairing_check")
     act = oc["mac_equiv"] * nloc / (k_tot * 1e-3) if oc else None
-    kk = {n: pmc(f"gsv::bn::{n}") for n in ("k_bn_prepare", "k_bn_miller", "k_bn_final")}
-    roof = {"bound": "valu", "unit": "TMAC/s", "achieved": round(ref_ach / 1e12, 3), "peak": round(PEAK_MAC / 1e12, 3),
-            "frac": round(ref_ach / PEAK_MAC, 4), "frac_reference_equiv": round(ref_ach / PEAK_MAC, 4),
+    kk = {n: pmc(f"gsv::bn::{n}", "pmc_pairing.json") for n in ("k_bn_prepare", "k_bn_miller", "k_bn_final")}
+    # headline = the v_mad_u64_u32 our kernels execute (frac_actual); the reference-equivalent figure
+    # counts the reference's 254-bit Order*Q subgroup work, which this path does not do, so it is kept
+    # apart
+    roof = {"bound": "valu", "unit": "TMAC/s", "achieved": round(act / 1e12, 3) if act else None,
+            "peak": round(PEAK_MAC / 1e12, 3), "frac": round(act / PEAK_MAC, 4) if act else None,
             "frac_actual": round(act / PEAK_MAC, 4) if act else None,
+            "achieved_reference_equiv": round(ref_ach / 1e12, 3), "frac_reference_equiv": round(ref_ach / PEAK_MAC, 4),
             "mac_equiv_per_check_reference": FP_MULS_PER_CHECK_REF * MACS_PER_FP_MUL,
             "mac_equiv_per_check_actual": oc["mac_equiv"] if oc else None,
             "fp_products_per_check_actual": oc.get("fp_products") if oc else None,
@@ -741,7 +764,7 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
                                     "subgroup check included); mac_equiv_per_check_actual = the v_mad_u64_u32 our "
                                     "kernels execute per check (9x29-bit F_p products 81 + Montgomery reductions 81; "
                                     "psi subgroup test, precomputed lines, multi-Miller loop; instrumented build, "
-                                    "profiles/r02/opcount.json)"}
+                                    "profiles/{ROUND}/opcount.json)".format(ROUND=ROUND)}
     out = {"checks_per_s": round(N_CHECKS * psteps / pdt, 1), "checks": N_CHECKS, "checks_per_rank": nloc,
            "pipeline_depth": depth,
            "pairs_per_check": 4, "roofline": roof, "ms_per_step": round(pdt / psteps * 1e3, 3),
@@ -755,7 +778,8 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
 # ----------------------------------------------------------------------------- CPU legs (rank 0, N = 1)
 def cpu_baselines(ctx, legs, st, res, info):
     """every leg's CPU side on the box's host cores, one core and all cores
-    (`threads_all_core` = the GPU's 16-CPU share).  Bounded samples of the same workloads."""
+    (`threads_all_core` = one GPU's share of an 8-GPU node, nproc / 8 threads; the box's cgroup CPU
+    quota is reported beside it).  Bounded samples of the same workloads."""
     from oracle import oracle as O
     th = info["threads_all_core"]
     out = {}
@@ -821,15 +845,16 @@ def cpu_baselines(ctx, legs, st, res, info):
                          "sample": f"1 / {nshard} shards of 8,192 txs: blob decode + Sender (reference crypto) + "
                                    "chunk root (restatement), one shard per thread"}
     if "pairing" in st:
-        hin = st["pairing"]["pin"][:16 * th].cpu().numpy()
-        pexp = st["pairing"]["pexp"][:16 * th].cpu().numpy()
+        n1, nN = 64, max(2048, 64 * th)
+        hin = st["pairing"]["pin"][:nN].cpu().numpy()
+        pexp = st["pairing"]["pexp"][:nN].cpu().numpy()
         v = [None] * len(hin)
-        t1 = _threads_run(lambda i: v.__setitem__(i, O.pairing_check(bytes(hin[i]))), list(range(16)), 1)
+        t1 = _threads_run(lambda i: v.__setitem__(i, O.pairing_check(bytes(hin[i]))), list(range(n1)), 1)
         tN = _threads_run(lambda i: v.__setitem__(i, O.pairing_check(bytes(hin[i]))), list(range(len(hin))), th)
-        assert [2 if x < 0 else x for x in v] == pexp.tolist(), "pairing oracle disagrees"
-        out["pairing"] = {"one_core": round(16 / t1, 1), "all_core": round(len(hin) / tN, 1), "unit": "checks/s",
-                          "kind": "port", "sample": f"16 / {len(hin)} 4-pair checks of the configs[4] workload, "
-                                                    "oracle restatement of crypto/bn256/cloudflare"}
+        assert [2 if x < 0 else x for x in v] == pexp[:len(v)].tolist(), "pairing oracle disagrees"
+        out["pairing"] = {"one_core": round(n1 / t1, 1), "all_core": round(len(hin) / tN, 1), "unit": "checks/s",
+                          "kind": "port", "sample": f"{n1} (1 thread) / {len(hin)} ({th} threads) 4-pair checks of the "
+                                                    "configs[4] workload, oracle restatement of crypto/bn256/cloudflare"}
     return out
 
 
@@ -896,6 +921,9 @@ def main():
         legs_cpu = cpu_baselines(ctx, legs, state, res, info)
         ec = legs_cpu.get("ecrecover")
         cpu = {"value": ec["all_core"] if ec else None, "unit": "sigs/s", "cores": info["threads_all_core"],
+               "threads": info["threads_all_core"],
+               "threads_basis": "one host thread per CPU of one GPU's share of an 8-GPU node (nproc / 8)",
+               "cgroup_cpu_quota": info["cgroup_cpu_quota"], "affinity_cpus": info["affinity"],
                "kind": ec["kind"] if ec else None, "sample": ec["sample"] if ec else None,
                "nproc": info["nproc"], "cpu_model": info["cpu_model"],
                "one_core": ec["one_core"] if ec else None, "all_core": ec["all_core"] if ec else None,

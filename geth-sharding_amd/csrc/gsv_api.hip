@@ -347,17 +347,6 @@ void shape_insert(gsv_ctx* c, std::unique_ptr<Shape> s) {
     }
 }
 
-// drops the cached shape `s` (after its queued work has drained)
-void shape_erase(gsv_ctx* c, Shape* s) {
-    for (auto it = c->shapes.begin(); it != c->shapes.end(); ++it)
-        if (it->get() == s) {
-            shape_drain(*s);
-            c->shape_bytes -= shape_total_bytes(*s);
-            c->shapes.erase(it);
-            return;
-        }
-}
-
 // The instance a run on `st` uses: the one last used on `st` (the stream orders it), else one never
 // used, else the next in turn, ordered after its previous use.  Inside a capture: the instance last
 // used on `st`, else instance 0 (the caller orders graph replays against other uses of the shape).
@@ -1165,8 +1154,11 @@ int partition_gather(gsv_ctx* c, const uint8_t* blk, uint8_t* all, const PartDim
 template <typename B>
 int shape_get(gsv_ctx* c, uint64_t kind, std::vector<uint64_t>&& key, B&& build, Shape** out) {
     Shape* s = shape_find(c, kind, key);
-    if (s && s->ninst < c->pipeline_depth) {  // prepared before the depth was raised: rebuild
-        shape_erase(c, s);
+    if (s && s->ninst < c->pipeline_depth) {
+        // prepared before the depth was raised: build a deeper one, and RETIRE the old one instead of
+        // freeing it (it is never found again but keeps its memory until LRU eviction, which drains
+        // its queued work first), so a graph captured from it stays valid until then
+        s->kind |= 1ull << 63;
         s = nullptr;
     }
     if (!s) {

@@ -231,8 +231,11 @@ MI30_FN void s30_to_words(uint32_t w[8], const s30& a) {
     }
 }
 
-// out = x^-1 mod m (x < m; 0 -> 0), words in and out
-MI30_FN void modinv30_words(uint32_t out[8], const uint32_t x[8], const modinfo30& mi) {
+// out = x^-1 mod m (x < m; 0 -> 0), words in and out.  VAR: variable-time divsteps (public inputs
+// only: the recovery path's r and Z); the constant-time form is used for a secret input (the
+// synthetic signer's nonce, modinv30_words_ct) whatever MI30_VAR says.
+template <bool VAR>
+MI30_FN void modinv30_words_t(uint32_t out[8], const uint32_t x[8], const modinfo30& mi) {
     GSV_OPC(gsv::OPC_MODINV);
     s30 d, e, f, g;
 #pragma unroll
@@ -243,7 +246,7 @@ MI30_FN void modinv30_words(uint32_t out[8], const uint32_t x[8], const modinfo3
     }
     e.v[0] = 1;
     s30_from_words(g, x);
-#if MI30_VAR
+    if constexpr (VAR) {
     // variable-time divsteps until g == 0 in every lane of the wave (a lane that is done keeps
     // d and f: its matrix is then diag(2^30, 1)); 25 batches cover the original divstep's bound
     // for 256-bit inputs (724), ~19 are typical
@@ -261,7 +264,7 @@ MI30_FN void modinv30_words(uint32_t out[8], const uint32_t x[8], const modinfo3
         for (int k = 0; k < 9; k++) gz |= (uint32_t)g.v[k];
         if (!MI30_ANY(gz != 0)) break;
     }
-#else
+    } else {
     int32_t zeta = -1;
 #if defined(__HIPCC__)
 #pragma unroll 1
@@ -272,9 +275,15 @@ MI30_FN void modinv30_words(uint32_t out[8], const uint32_t x[8], const modinfo3
         mi30_update_de(d, e, t, mi);
         mi30_update_fg(f, g, t);
     }
-#endif
+    }
     mi30_normalize(d, f.v[8], mi);
     s30_to_words(out, d);
+}
+MI30_FN void modinv30_words(uint32_t out[8], const uint32_t x[8], const modinfo30& mi) {
+    modinv30_words_t<MI30_VAR != 0>(out, x, mi);
+}
+MI30_FN void modinv30_words_ct(uint32_t out[8], const uint32_t x[8], const modinfo30& mi) {
+    modinv30_words_t<false>(out, x, mi);
 }
 
 }  // namespace gsv

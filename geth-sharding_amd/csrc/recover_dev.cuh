@@ -65,6 +65,12 @@ constexpr int GSV_LTAB_WORDS = 18 * GLV_LNT * GSV_LTAB_STRIDE;
 #ifndef GSV_GLV_BETA_TAB
 #define GSV_GLV_BETA_TAB 0
 #endif
+// 1: the private-array half of the GLV table is read one add AHEAD (software prefetch): its scratch
+// loads (L2/MALL latency) run under the current add instead of stalling it; every lane reads both
+// halves at index (e & 3) and selects (no divergent branch).  GSV_GLV_TAB == 2 only.
+#ifndef GSV_GLV_PREFETCH
+#define GSV_GLV_PREFETCH 0
+#endif
 // 1: the two adds of a digit position (k1 on T, k2 on lambda T) as straight-line code (A/B)
 #ifndef GSV_GLV_UNROLL_J
 #define GSV_GLV_UNROLL_J 0
@@ -457,6 +463,62 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         acc.y.v[k] = GLV_Y(0, k);
     }
     fe9_set_u32(acc.z, 1);
+#if GSV_GLV_PREFETCH && GSV_GLV_TAB == 2 && !GSV_GLV_BETA_TAB
+    static_assert(GLV_LNT == 4 && PNT == 4, "prefetch layout: entries 0-3 in LDS, 4-7 private");
+    {
+        constexpr uint32_t CMASK = (1u << DIG_SLOT) - 1u;
+        auto code_at = [&](int i, int j) -> uint32_t {
+            return (sel_word(j ? dig2 : dig1, (uint32_t)i / DIG_PER_WORD) >> ((i % DIG_PER_WORD) * DIG_SLOT)) & CMASK;
+        };
+        uint32_t pre[18];
+        auto prefetch = [&](uint32_t c) {
+            uint32_t xo = (c & 3u) * 9u;
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                pre[k] = ptab[xo + k];
+                pre[9 + k] = ptab[9 * PNT + xo + k];
+            }
+        };
+        uint32_t cn = code_at(GLV_DIGITS - 1, 0);
+        prefetch(cn);
+#pragma unroll 1
+        for (int i = GLV_DIGITS - 1; i >= 0; i--) {
+            if (i != GLV_DIGITS - 1) {
+#pragma unroll 1
+                for (int d = 0; d < GLV_W; d++) gej9_dbl(acc, acc);
+            }
+#pragma unroll 1
+            for (int j = 0; j < 2; j++) {
+                uint32_t c = cn;
+                bool ng = j ? neg2 : neg1;
+                uint32_t ei = c & (uint32_t)(GLV_NT - 1);
+                bool hi = ei >= 4u;
+                uint32_t xo = (ei & 3u) * 9u;
+                ge9 P;
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    uint32_t lx = GLV_L(xo + k), ly = GLV_L(9u * GLV_LNT + xo + k);
+                    P.x.v[k] = hi ? pre[k] : lx;
+                    P.y.v[k] = hi ? pre[9 + k] : ly;
+                }
+                int ni = j ? i - 1 : i;  // the next add: (i, 1) or (i - 1, 0)
+                if (ni >= 0) {           // wave-uniform
+                    cn = code_at(ni, j ? 0 : 1);
+                    prefetch(cn);
+                }
+                if (j != 0) {  // wave-uniform
+                    fe9 beta;
+                    fe9_from_const(beta, BETA);
+                    fe9_mul(P.x, P.x, beta);
+                }
+                fe9 ny;
+                fe9_neg<1>(ny, P.y);
+                fe9_cmov(P.y, ny, ((c >> (GLV_W - 1)) != 0) != ng);
+                gej9_add_ge(acc, ainf, acc, P);
+            }
+        }
+    }
+#else
 #pragma unroll 1
     for (int i = GLV_DIGITS - 1; i >= 0; i--) {
         if (i != GLV_DIGITS - 1) {
@@ -508,6 +570,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             gej9_add_ge(acc, ainf, acc, P);
         }
     }
+#endif
     // skew corrections: the recoded scalars were k + skew -> subtract (+-)T0 / (+-)lambda(T0)
 #pragma unroll 1
     for (int j = 0; j < 2; j++) {
@@ -629,7 +692,7 @@ GSV_DI void ecdsa_sign(uint32_t r_out[8], uint32_t s_out[8], uint32_t& recid, fe
     if (over) recid |= 2u;
     // s = k^-1 (m + r d)
     sc kinv, s, t;
-    modinv30_words(kinv.v, k.v, MI30_N);
+    modinv30_words_ct(kinv.v, k.v, MI30_N);  // the nonce is secret: constant-time divsteps
     sc_mul(t, r, d);
     sc_add(t, t, mr);
     sc_mul(s, kinv, t);

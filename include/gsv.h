@@ -128,7 +128,10 @@ int gsv_ctx_prepared_shapes(gsv_ctx *ctx, size_t *count, size_t *device_bytes);
 /* Pipeline depth D (1..GSV_MAX_PIPELINE_DEPTH, default 1) of the shapes prepared from now on: each
  * holds D instances of its device memory (tables and workspace), so *_dev calls of ONE shape on up to
  * D different streams run concurrently instead of being ordered after each other (a stream keeps
- * the instance it last used).  A shape prepared at a lower depth is rebuilt by its next prepare.
+ * the instance it last used).  A shape prepared at a lower depth is replaced by its next prepare
+ * (including the implicit prepare of a binding's *_dev wrapper): the new, deeper shape serves the
+ * later calls, and the old one is retired, not freed — its memory stays valid (a HIP graph captured
+ * from it can still be replayed) until the shape cache's LRU bound evicts it, after its queued work.
  * Use: validating consecutive batches of equal shape on two streams overlaps one batch's
  * latency-bound tail (trie top, final exponentiation) with the next batch's bulk kernels. */
 #define GSV_MAX_PIPELINE_DEPTH 8

@@ -55,7 +55,7 @@ def main(root):
     write = counters(os.path.join(root, "write", "run_results.db"), {"WRITE_SIZE"})
     sq = counters(os.path.join(root, "sq", "run_results.db"),
                   {"SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
-                   "GRBM_GUI_ACTIVE"})
+                   "GRBM_GUI_ACTIVE", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"})
     ipath = os.path.join(root, "int", "run_results.db")
     ints = counters(ipath, {"SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64"}) if os.path.exists(ipath) else {}
     for k in sorted(set(dur) | set(fetch)):
@@ -84,6 +84,14 @@ def main(root):
                 # GRBM_GUI_ACTIVE sums the 8 XCDs' clocks; each of the 1024 SIMDs issues at most one
                 # wave-instruction per cycle: VALU wave-instructions per SIMD per cycle
                 r["valu_issue_per_simd_cycle"] = round(r["sq_insts_valu"] / (1024 * gui / 8), 4)
+                r["gpu_cycles_per_dispatch"] = round(gui / 8)
+                if r.get("avg_ms"):  # effective clock of the profiled run (MI355X_MICROARCH.md, DVFS)
+                    r["profiled_clock_ghz"] = round(gui / 8 / (r["avg_ms"] * 1e6), 3)
+            if wcyc:  # where the waves' cycles went (disjoint buckets, quad-cycle units)
+                for key, name in (("SQ_WAIT_ANY", "wait_any_frac"), ("SQ_WAIT_INST_ANY", "wait_inst_any_frac"),
+                                  ("SQ_ACTIVE_INST_ANY", "active_inst_any_frac")):
+                    if s.get(key):
+                        r[name] = round(per_dispatch(s[key]) / wcyc, 4)
         i = ints.get(k, {})
         if i.get("SQ_INSTS_VALU_INT32"):
             r["sq_insts_valu_int32"] = per_dispatch(i["SQ_INSTS_VALU_INT32"])
