@@ -291,9 +291,15 @@ def cpu_sender(threads_all):
     off[1:] = np.cumsum([len(t) for t in txs])
     res = {}
     for label, th in (("one_core", 1), ("all_core", threads_all)):
-        addr, st, dt = cfg0.sender_many(flat, off, len(txs), th)
-        assert (st == 0).all() and (addr == want_addr).all(), "CPU Sender disagrees with the signer"
-        res[label] = round(len(txs) / dt, 1)
+        # repeat the 10k-tx batch until >= 1 s has passed: a shorter burst runs inside one period of
+        # the box's cgroup CPU quota and reads above the sustained rate
+        n_done, t_sum = 0, 0.0
+        while t_sum < 1.0:
+            addr, st, dt = cfg0.sender_many(flat, off, len(txs), th)
+            assert (st == 0).all() and (addr == want_addr).all(), "CPU Sender disagrees with the signer"
+            n_done += len(txs)
+            t_sum += dt
+        res[label] = round(n_done / t_sum, 1)
     O.lib().oracle_set_crypto(None, None)
     return res, kind, (txs, want_addr)
 
@@ -808,15 +814,17 @@ def cpu_baselines(ctx, legs, st, res, info):
     del flat
     if "chunk_root" in st:
         cb = st["chunk_root"]["bodies"]
-        bodies = [cb[i * BODY:(i + 1) * BODY].cpu().numpy().tobytes() for i in range(th)]
-        roots = [None] * th
+        nbd = min(N_SHARDS, 2 * th)  # two bodies per thread: >= 1 s of sustained work
+        bodies = [cb[i * BODY:(i + 1) * BODY].cpu().numpy().tobytes() for i in range(nbd)]
+        roots = [None] * nbd
         t1 = _threads_run(lambda i: roots.__setitem__(i, O.derive_sha_bytes(bodies[i])), [0], 1)
-        tN = _threads_run(lambda i: roots.__setitem__(i, O.derive_sha_bytes(bodies[i])), list(range(th)), th)
-        gr = st["chunk_root"]["roots"][:th].cpu().numpy()
-        assert all(roots[i] == bytes(gr[i]) for i in range(th)), "chunk root mismatch vs oracle"
-        out["chunk_root"] = {"one_core": round(BODY / t1 / 1e9, 4), "all_core": round(th * BODY / tN / 1e9, 4),
+        tN = _threads_run(lambda i: roots.__setitem__(i, O.derive_sha_bytes(bodies[i])), list(range(nbd)), th)
+        gr = st["chunk_root"]["roots"][:nbd].cpu().numpy()
+        assert all(roots[i] == bytes(gr[i]) for i in range(nbd)), "chunk root mismatch vs oracle"
+        out["chunk_root"] = {"one_core": round(BODY / t1 / 1e9, 4), "all_core": round(nbd * BODY / tN / 1e9, 4),
                              "unit": "GB/s of collation body", "kind": "port",
-                             "sample": f"1 / {th} bodies of 1 MiB (one per thread), oracle DeriveSha restatement"}
+                             "sample": f"1 body (1 thread) / {nbd} bodies ({th} threads) of 1 MiB, oracle DeriveSha "
+                                       "restatement"}
     if "notary" in st:
         from oracle import cfg0
         cfg0.use_reference_crypto()

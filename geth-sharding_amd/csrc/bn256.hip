@@ -408,6 +408,11 @@ static BN_NI bool g2_in_subgroup(const g2a* pq) {
 
 // ---------------------------------------------------------------- Miller loop (optate.go)
 struct line { fp2 a, b, c; };
+// 1: the line role's formulas ordered / fed for register pressure (pair_lines, line_double_i); the
+// field elements are the same
+#ifndef BN_LINES_LEAN
+#define BN_LINES_LEAN 1
+#endif
 // optate.go:3-50 (mixed addition r + p, p affine with t = 1; r2 = p.y^2)
 GSV_DI line line_add_i(g2j& r, const g2a& p, const g1a& q, const fp2& r2) {
     fp2 B = s2(fp2_mul(p.x, r.t));
@@ -438,15 +443,27 @@ GSV_DI line line_double_i(g2j& r, const g1a& q) {
     fp2 D = s2(fp2_dbl(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.x, B)), A), C)));
     fp2 E = s2(fp2_add(fp2_dbl(A), A));
     fp2 G = s2(fp2_sqr(E));
+    line l;
     g2j o;
+#if BN_LINES_LEAN
+    // the same values in the order that ends each input's life earliest (r.x with l.a, r.y / r.z / B
+    // with o.z, r.t with l.b / l.c), against the line role's register pressure
+    l.a = s2(fp2_sub(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.x, E)), A), G), fp2_mul_small<4>(B)));
+    o.z = s2(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.y, r.z)), B), r.t));
+    l.b = s2(fp2_mul_fp(fp2_neg(fp2_dbl(fp2_mul(E, r.t))), q.x));
+    l.c = s2(fp2_mul_fp(fp2_dbl(fp2_mul(o.z, r.t)), q.y));
+    o.x = s2(fp2_sub(G, fp2_dbl(D)));
+    o.y = s2(fp2_sub(fp2_mul(fp2_sub(D, o.x), E), fp2_mul_small<8>(C)));
+    o.t = s2(fp2_sqr(o.z));
+#else
     o.x = s2(fp2_sub(G, fp2_dbl(D)));
     o.z = s2(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.y, r.z)), B), r.t));
     o.y = s2(fp2_sub(fp2_mul(fp2_sub(D, o.x), E), fp2_mul_small<8>(C)));
     o.t = s2(fp2_sqr(o.z));
-    line l;
     l.b = s2(fp2_mul_fp(fp2_neg(fp2_dbl(fp2_mul(E, r.t))), q.x));
     l.a = s2(fp2_sub(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.x, E)), A), G), fp2_mul_small<4>(B)));
     l.c = s2(fp2_mul_fp(fp2_dbl(fp2_mul(o.z, r.t)), q.y));
+#endif
     r = o;
     return l;
 }
@@ -597,15 +614,29 @@ enum : uint8_t { PS_OK = 0, PS_SKIP = 1, PS_BAD = 2 };
 // multiplies them in.  Lines of an invalid or infinite pair are computed but never used.
 GSV_DI void pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j, const g1a& P, const g2a& Q) {
     g2j r{Q.x, Q.y, fp2_one(), fp2_one()};
+    int li = 0;
+#if BN_LINES_LEAN
+    // -Q and r2 = Q.y^2 are formed at each addition step (27 of the 91) instead of living in VGPRs
+    // through all of them: 36 fewer registers held against the line role's spills
+#pragma unroll 1
+    for (int i = 64; i > 0; i--) {
+        line_store(lines, npairs, j, li++, line_double_i(r, P));
+        uint64_t bit = 1ull << (i - 1);
+        if ((NAF_POS | NAF_NEG) & bit) {
+            g2a q{Q.x, (NAF_POS & bit) ? Q.y : s2(fp2_neg(Q.y))};
+            line_store(lines, npairs, j, li++, line_add_i(r, q, P, s2(fp2_sqr(Q.y))));
+        }
+    }
+#else
     fp2 r2 = s2(fp2_sqr(Q.y));
     g2a mQ{Q.x, s2(fp2_neg(Q.y))};
-    int li = 0;
 #pragma unroll 1
     for (int i = 64; i > 0; i--) {
         line_store(lines, npairs, j, li++, line_double_i(r, P));
         uint64_t bit = 1ull << (i - 1);
         if ((NAF_POS | NAF_NEG) & bit) line_store(lines, npairs, j, li++, line_add_i(r, (NAF_POS & bit) ? Q : mQ, P, r2));
     }
+#endif
     // Q1 = pi(Q), -Q2 = -pi^2(Q) (optate.go:168-209)
     g2a q1{s2(fp2_mul(fp2_conj(Q.x), fp2_const(FQ_XI_P1_3_X, FQ_XI_P1_3_Y))),
            s2(fp2_mul(fp2_conj(Q.y), fp2_const(FQ_XI_P1_2_X, FQ_XI_P1_2_Y)))};
@@ -614,9 +645,12 @@ GSV_DI void pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j
     line_store(lines, npairs, j, li, line_add_i(r, mq2, P, s2(fp2_sqr(mq2.y))));
 }
 
-// role 0 (checks) / role 1 (lines) of pair i
+// role 0 (checks) / role 1 (lines) of pair i.  With `luse` (the concurrent layout) the lines role also
+// writes whether the Miller loop uses the pair's lines: PS_OK for a decoded pair with neither point at
+// infinity, PS_SKIP otherwise; the curve / subgroup verdict (pstat) then arrives only for k_bn_final.
 GSV_DI void prepare_pair(bool role_lines, uint32_t i, const uint8_t* __restrict__ in, const uint64_t* __restrict__ pair_src,
-                         uint32_t npairs, uint8_t* __restrict__ pstat, uint32_t* __restrict__ lines) {
+                         uint32_t npairs, uint8_t* __restrict__ pstat, uint32_t* __restrict__ lines,
+                         uint8_t* __restrict__ luse = nullptr) {
     const uint8_t* s = in + pair_src[i];
     g1a P;
     g2a Q;
@@ -626,12 +660,13 @@ GSV_DI void prepare_pair(bool role_lines, uint32_t i, const uint8_t* __restrict_
     ok = fp_unmarshal(Q.x.y, s + 96) && ok;
     ok = fp_unmarshal(Q.y.x, s + 128) && ok;
     ok = fp_unmarshal(Q.y.y, s + 160) && ok;
+    bool inf1 = fq_is_zero(P.x) && fq_is_zero(P.y);
+    bool inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
     if (role_lines) {
+        if (luse) luse[i] = ok && !inf1 && !inf2 ? PS_OK : PS_SKIP;
         pair_lines(lines, npairs, i, P, Q);
         return;
     }
-    bool inf1 = fq_is_zero(P.x) && fq_is_zero(P.y);
-    bool inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
     if (ok && !inf1)  // curve.go:39-52: y^2 == x^3 + 3
         ok = fq_eq(fq_mul(P.y, P.y), fq_add(fq_mul(fq_mul(P.x, P.x), P.x), fq_const(FQ_THREE)));
     if (ok && !inf2) ok = g2_in_subgroup(&Q);
@@ -671,9 +706,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVE
 }
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_LINES_WAVES))) void k_bn_lines(const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ pair_src,
-                                                   uint32_t npairs, uint32_t* __restrict__ lines) {
+                                                   uint32_t npairs, uint32_t* __restrict__ lines,
+                                                   uint8_t* __restrict__ luse) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, nullptr, lines);
+    if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, nullptr, lines, luse);
 }
 
 // ---- per-check multi-Miller loop.  The product of a check's Miller values equals one loop that
@@ -895,12 +931,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
 // role/base as final_exp: the verdict is written by role 0
 // cbad[c] != 0: the check's input length is not a multiple of 192 (errBadPairingInput,
 // core/vm/contracts.go:336-338); it has no pairs
+// PairBad (concurrent layout): the check kernel's per-pair verdicts, read here because the Miller
+// loop ran on the lines role's PS_OK / PS_SKIP alone
+struct PairBad {
+    const uint32_t* lane_first;
+    const uint32_t* pidx;
+    const uint8_t* pstat;  // nullptr: the Miller loop already saw pstat (lstat CS_BAD)
+};
 GSV_DI void final_check(uint32_t c, const uint32_t* __restrict__ check_lane, const uint8_t* __restrict__ cbad,
                         const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv, uint32_t nlanes,
-                        uint8_t* __restrict__ verdict, int role, int base) {
+                        uint8_t* __restrict__ verdict, int role, int base, const PairBad& pb) {
     uint32_t l0 = check_lane[c], l1 = check_lane[c + 1];
     bool bad = cbad[c] != 0;
     for (uint32_t l = l0; l < l1; l++) bad = bad || lstat[l] == CS_BAD;
+    if (pb.pstat)
+        for (uint32_t q = pb.lane_first[l0]; q < pb.lane_first[l1]; q++) bad = bad || pb.pstat[pb.pidx[q]] == PS_BAD;
     if (bad) {
         if (role == 0) verdict[c] = GSV_PAIRING_BAD_INPUT;
         return;
@@ -926,21 +971,21 @@ GSV_DI void final_check(uint32_t c, const uint32_t* __restrict__ check_lane, con
 __global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
                                                  const uint8_t* __restrict__ cbad, const uint8_t* __restrict__ lstat,
                                                  const uint32_t* __restrict__ fv, uint32_t nlanes,
-                                                 uint8_t* __restrict__ verdict) {
+                                                 uint8_t* __restrict__ verdict, PairBad pb) {
     uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchecks) return;
-    final_check(c, check_lane, cbad, lstat, fv, nlanes, verdict, 0, -1);
+    final_check(c, check_lane, cbad, lstat, fv, nlanes, verdict, 0, -1, pb);
 }
 // three lanes per check (21 triples per wave, lane 63 idle); a triple's lanes take the same path
 constexpr uint32_t FINAL3_PER_WAVE = 21;
 __global__ __launch_bounds__(64) void k_bn_final3(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
                                                   const uint8_t* __restrict__ cbad, const uint8_t* __restrict__ lstat,
                                                   const uint32_t* __restrict__ fv, uint32_t nlanes,
-                                                  uint8_t* __restrict__ verdict) {
+                                                  uint8_t* __restrict__ verdict, PairBad pb) {
     int t = threadIdx.x / 3, role = threadIdx.x - 3 * t;
     uint32_t c = blockIdx.x * FINAL3_PER_WAVE + t;
     if (t >= (int)FINAL3_PER_WAVE || c >= nchecks) return;
-    final_check(c, check_lane, cbad, lstat, fv, nlanes, verdict, role, 3 * t);
+    final_check(c, check_lane, cbad, lstat, fv, nlanes, verdict, role, 3 * t, pb);
 }
 
 
@@ -1105,14 +1150,33 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
                                 uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
                                 uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
-                                void (*timer_end)(void*, int), void* tctx) {
-    if (npairs) {
+                                void (*timer_end)(void*, int), void* tctx, const BnConcurrent* conc) {
+    // GSV_BN_LAYOUT_CONC: the curve / subgroup checks run on a side stream beside the lines, the Miller
+    // loop (on the lines role's PS_OK / PS_SKIP) and join before the final exponentiation, which reads
+    // their verdicts; the lines kernel has a one-wave register budget (no spills).  For batches that
+    // leave SIMDs idle: the check waves fill them.
+    const bool cc = (layout & GSV_BN_LAYOUT_CONC) && conc && npairs;
+    bn::PairBad pb{d_lane_first, d_pidx, cc ? d_pstat : nullptr};
+    const uint8_t* d_use = cc ? conc->d_luse : d_pstat;
+    if (cc) {
+        if (hipEventRecord(conc->fork, st) != hipSuccess || hipStreamWaitEvent(conc->side, conc->fork, 0) != hipSuccess)
+            return hipErrorUnknown;
+        hipLaunchKernelGGL(bn::k_bn_check, dim3((npairs + 63) / 64), dim3(64), 0, conc->side, d_in, d_pair_src, npairs,
+                           d_pstat);
+        if (hipEventRecord(conc->join, conc->side) != hipSuccess) return hipErrorUnknown;
+        if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
+        hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
+                           d_lines, conc->d_luse);
+        if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    } else if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
         if (BN_PREP_SPLIT) {
             hipLaunchKernelGGL(bn::k_bn_check, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
                                d_pstat);
             hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                               d_lines);
+                               d_lines, (uint8_t*)nullptr);
         } else {
             hipLaunchKernelGGL(bn::k_bn_prepare, dim3(2 * ((npairs + 63) / 64)), dim3(64), 0, st, d_in, d_pair_src,
                                npairs, d_pstat, d_lines);
@@ -1128,21 +1192,24 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
         if (layout & GSV_BN_LAYOUT_MILLER2)
             hipLaunchKernelGGL(bn::k_bn_miller2, dim3((2 * nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
-                               d_pidx, d_pstat, d_lines, npairs, d_lstat, d_fv);
+                               d_pidx, d_use, d_lines, npairs, d_lstat, d_fv);
         else
             hipLaunchKernelGGL(bn::k_bn_miller, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
-                               d_pidx, d_pstat, d_lines, npairs, d_lstat, d_fv);
+                               d_pidx, d_use, d_lines, npairs, d_lstat, d_fv);
         if (timer_end) timer_end(tctx, GSV_K_PAIRING);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+        if (cc && hipStreamWaitEvent(st, conc->join, 0) != hipSuccess) return hipErrorUnknown;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
         if (layout & GSV_BN_LAYOUT_FINAL3)
             hipLaunchKernelGGL(bn::k_bn_final3, dim3((nchecks + bn::FINAL3_PER_WAVE - 1) / bn::FINAL3_PER_WAVE),
-                               dim3(64), 0, st, d_check_lane, nchecks, d_cbad, d_lstat, d_fv, nlanes, d_verdict);
+                               dim3(64), 0, st, d_check_lane, nchecks, d_cbad, d_lstat, d_fv, nlanes, d_verdict, pb);
         else
             hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_lane, nchecks,
-                               d_cbad, d_lstat, d_fv, nlanes, d_verdict);
+                               d_cbad, d_lstat, d_fv, nlanes, d_verdict, pb);
         if (timer_end) timer_end(tctx, GSV_K_BN_FINAL);
+    } else if (cc && hipStreamWaitEvent(st, conc->join, 0) != hipSuccess) {
+        return hipErrorUnknown;
     }
     return hipGetLastError();
 }

@@ -809,7 +809,10 @@ struct TopLevels {
 };
 constexpr uint32_t TOP_MAX_BODIES = 256;  // one fused-top workgroup per CU at most
 constexpr int TOP_HFULL_THREADS = 256;  // waves 0-3: HFULL nodes, one per lane
-constexpr int TOP_GEN_WAVES = 2;        // waves 4-5: generic nodes, one per wave (never behind HFULL work)
+#ifndef GSV_TOP_GEN_WAVES
+#define GSV_TOP_GEN_WAVES 2
+#endif
+constexpr int TOP_GEN_WAVES = GSV_TOP_GEN_WAVES;  // waves 4..: generic nodes, one per wave (never behind HFULL work)
 constexpr int TOP_BLOCK = TOP_HFULL_THREADS + 64 * TOP_GEN_WAVES;
 
 // one workgroup per body, a barrier between heights (children's hashes are in the CU's L1/L2).

@@ -90,7 +90,10 @@ struct Shape {
     size_t np = 0, nl = 0, nchecks = 0;
     int layout = 0;  // GSV_BN_LAYOUT_* flags
     size_t o_src = 0, o_pidx = 0, o_lfirst = 0, o_clane = 0, o_cbad = 0, o_pstat = 0, o_lines = 0,
-           o_lstat = 0, o_fv = 0;
+           o_lstat = 0, o_fv = 0, o_luse = 0;
+    // GSV_BN_LAYOUT_CONC: per instance, the side stream and fork/join events (created at prepare)
+    std::vector<hipStream_t> side;
+    std::vector<hipEvent_t> efork, ejoin;
     // SK_NOTARY
     uint32_t max_txs = 0, sfx_len = 0;
     int signer_kind = 0;
@@ -114,6 +117,12 @@ struct Shape {
     Shape(const Shape&) = delete;
     Shape& operator=(const Shape&) = delete;
     ~Shape() {
+        for (hipEvent_t e : efork)
+            if (e) hipEventDestroy(e);
+        for (hipEvent_t e : ejoin)
+            if (e) hipEventDestroy(e);
+        for (hipStream_t q : side)
+            if (q) hipStreamDestroy(q);
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : bulk_ev)
@@ -794,6 +803,13 @@ bool bn_miller2(size_t nlanes, int cus) {
     if (const char* e = getenv("GSV_BN_MILLER2")) return atoi(e) != 0;
     return 2 * nlanes <= (size_t)std::max(cus, 1) * 4 * 64;
 }
+// Curve / subgroup checks on a side stream beside the lines and the Miller loop (GSV_BN_LAYOUT_CONC):
+// pays while the lines and Miller waves leave SIMDs idle, i.e. below about one Miller wave per SIMD.
+// GSV_BN_CONC = 0/1 forces the choice (A/B timing).
+bool bn_conc(size_t npairs, int cus) {
+    if (const char* e = getenv("GSV_BN_CONC")) return atoi(e) != 0;
+    return npairs <= (size_t)std::max(cus, 1) * 4 * 64 * 1;
+}
 // Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
 // lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
 // and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
@@ -819,7 +835,9 @@ std::vector<uint64_t> pairing_key(const uint64_t* h_off, size_t n) {
     const char* k = getenv("GSV_BN_PAIRS_PER_LANE");
     const char* f = getenv("GSV_BN_FINAL3");
     const char* m = getenv("GSV_BN_MILLER2");
-    std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0, m ? (uint64_t)atoi(m) + 1 : 0};
+    const char* cc = getenv("GSV_BN_CONC");
+    std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0, m ? (uint64_t)atoi(m) + 1 : 0,
+                              cc ? (uint64_t)atoi(cc) + 1 : 0};
     key.insert(key.end(), h_off, h_off + n + 1);
     return key;
 }
@@ -883,7 +901,8 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.nl = lane_first.size() - 1;
     s.nchecks = n;
     s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
-               (bn_miller2(s.nl, cus) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0);
+               (bn_miller2(s.nl, cus) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
+               (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0);
     s.o_src = L.add(np * 8 + 8);
     s.o_pidx = L.add(np * 4 + 4);
     s.o_lfirst = L.add((s.nl + 1) * 4);
@@ -892,6 +911,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.o_pstat = L.add(np + 1);
     s.o_lines = L.add(np * 91 * 54 * 4 + 4);  // the pairs' Miller-loop lines (bn256.hip BN_NLINES)
     s.o_lstat = L.add(s.nl + 1);
+    s.o_luse = L.add(np + 1);
     s.o_fv = L.add(s.nl * 108 * 4 + 4);
     s.stage(s.o_src, pair_src.data(), np);
     s.stage(s.o_pidx, pidx.data(), np);
@@ -900,12 +920,32 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.stage(s.o_cbad, bad_len.data(), n);
     return GSV_SUCCESS;
 }
+// the concurrent layout's side streams and events, one set per instance (at prepare / host-path build)
+int pairing_conc_init(Shape& s) {
+    if (!(s.layout & gsv::GSV_BN_LAYOUT_CONC) || !s.side.empty()) return GSV_SUCCESS;
+    s.side.assign(s.ninst, nullptr);
+    s.efork.assign(s.ninst, nullptr);
+    s.ejoin.assign(s.ninst, nullptr);
+    for (int k = 0; k < s.ninst; k++) {
+        HIPCHK(hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&s.efork[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&s.ejoin[k], hipEventDisableTiming));
+    }
+    return GSV_SUCCESS;
+}
 int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verdict, hipStream_t st) {
+    gsv::BnConcurrent conc{};
+    const gsv::BnConcurrent* pc = nullptr;
+    if ((s.layout & gsv::GSV_BN_LAYOUT_CONC) && (size_t)s.cur < s.side.size()) {
+        conc = gsv::BnConcurrent{s.side[s.cur], s.efork[s.cur], s.ejoin[s.cur], s.at<uint8_t>(s.o_luse)};
+        pc = &conc;
+    }
+    int layout = pc ? s.layout : (s.layout & ~gsv::GSV_BN_LAYOUT_CONC);
     return hip_err(gsv::launch_bn256_pairing(
         d_in, s.at<uint64_t>(s.o_src), (uint32_t)s.np, s.at<uint32_t>(s.o_lfirst), s.at<uint32_t>(s.o_pidx),
         (uint32_t)s.nl, s.at<uint32_t>(s.o_clane), s.at<uint8_t>(s.o_cbad), (uint32_t)s.nchecks,
         s.at<uint8_t>(s.o_pstat), s.at<uint32_t>(s.o_lines), s.at<uint8_t>(s.o_lstat),
-        s.at<uint32_t>(s.o_fv), d_verdict, s.layout, st, hook_begin, hook_end, c));
+        s.at<uint32_t>(s.o_fv), d_verdict, layout, st, hook_begin, hook_end, c, pc));
 }
 
 // ---- notary: key = chain id, signer, max_txs, body offsets
@@ -1363,8 +1403,10 @@ int gsv_bn256_pairing_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n) {
     std::lock_guard<std::mutex> g(c->smu);
     HIPCHK(hipSetDevice(c->device));
     Shape* s;
-    return shape_get(c, SK_PAIRING, pairing_key(h_off, n),
-                     [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, h_off, n, L); }, &s);
+    int rc = shape_get(c, SK_PAIRING, pairing_key(h_off, n),
+                       [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, h_off, n, L); }, &s);
+    if (rc) return rc;
+    return pairing_conc_init(*s);
 }
 
 int gsv_bn256_pairing_check_batch_dev(gsv_ctx* c, const uint8_t* d_in, const uint64_t* h_off, size_t n,
@@ -1397,6 +1439,8 @@ int gsv_bn256_pairing_check_batch(gsv_ctx* c, const uint8_t* in, const uint64_t*
     size_t staged = al(bytes + 8) + al(n);
     Shape s;
     int rc = shape_temp(c, staged, [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, rel.data(), n, L); }, s);
+    if (rc) return rc;
+    rc = pairing_conc_init(s);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_in = cv.take<uint8_t>(bytes + 8);

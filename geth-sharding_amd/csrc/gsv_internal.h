@@ -55,7 +55,13 @@ hipError_t launch_header_verify(const uint8_t* d_sid32, const uint8_t* d_root32,
 
 // layout flags of launch_bn256_pairing: the final exponentiation on three lanes per check, the Miller
 // loop on two lanes per Miller lane (both for batches below one wave per SIMD)
-constexpr int GSV_BN_LAYOUT_FINAL3 = 1, GSV_BN_LAYOUT_MILLER2 = 2;
+constexpr int GSV_BN_LAYOUT_FINAL3 = 1, GSV_BN_LAYOUT_MILLER2 = 2, GSV_BN_LAYOUT_CONC = 4;
+// the concurrent layout's side stream, fork/join events and the lines role's per-pair use flags
+struct BnConcurrent {
+    hipStream_t side;
+    hipEvent_t fork, join;
+    uint8_t* d_luse;
+};
 // bn256.hip: pairs in slot-major order (the j-th pairs of all checks contiguous): pair_src[p] = byte
 // offset of pair p in d_in.  A check's pairs are split into Miller lanes of <= k pairs each: lane l
 // runs the multi-Miller loop over pidx[lane_first[l] .. lane_first[l+1]), check c owns lanes
@@ -68,7 +74,7 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
                                 uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
                                 uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
-                                void (*timer_end)(void*, int), void* tctx);
+                                void (*timer_end)(void*, int), void* tctx, const BnConcurrent* conc);
 
 hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st);
 

@@ -1,8 +1,11 @@
-# A/B of the pairing leg: base library and any variants/<name>/libgsv.so given as arguments
+#!/bin/bash
+# A/B of the pairing leg: the in-tree library and variants/<name>/libgsv.so (pairing GPU tests first),
+# then the bench's pairing leg, alternating, 2 runs each.  GPU box, repo root.
 set -o pipefail
-A="--steps 2 --warmup 1 --no-cpu-baseline --no-chunk-leg --no-notary-leg --no-extra-legs"
-for v in base "$@"; do
-  if [ $v = base ]; then L=""; else L="variants/$v/libgsv.so"; fi
-  GSV_LIB_PATH=$L timeout -k 10 200 python -u bench.py $A > gpurun_out/ab_$v.log 2>&1 || exit 1
-  tail -1 gpurun_out/ab_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); p=d['bn256_pairing']; print('$v', p['checks_per_s'], p['prepare_kernel_ms'], p['miller_kernel_ms'], p['final_exp_kernel_ms'])"
+O=gpurun_out/abpair
+mkdir -p $O
+for v in main "$@"; do
+  if [ $v = main ]; then L=""; else L="variants/$v/libgsv.so"; fi
+  GSV_LIB_PATH=$L timeout -k 10 300 python -u -m pytest tests/test_gpu_bn256.py -x -q --timeout 160 --timeout-method thread > $O/test_$v.log 2>&1 || { echo "$v tests failed"; exit 1; }
 done
+AB_ARGS="--steps 12" timeout -k 10 600 python tools/ab_variants.py pairing main "$@" main "$@" | tee $O/summary.txt || exit 1
