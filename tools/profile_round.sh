@@ -9,15 +9,21 @@
 #        SQ_* VALU / wait counters + GRBM_GUI_ACTIVE                  -> issue rate, clock, stalls
 #        SQ_INSTS_VALU_INT32 / _INT64                                 -> integer VALU instructions
 # Output under gpurun_out/prof/<tag>/; summarised by tools/pmc_summary.py into pmc_<G>.json.
+#   tools/profile_round.sh <tag> [groups...]   (default: all ecrecover chunk_root keccak pairing notary)
 set -u
 TAG=${1:-r03}
+shift || true
+GROUPS_=${*:-all ecrecover chunk_root keccak pairing notary}
 OUT=gpurun_out/prof/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f rocpd csv -d $OUT/all/trace -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
-find $OUT/all/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
-for G in ecrecover chunk_root keccak pairing notary; do
+for G in $GROUPS_; do
+    if [ $G = all ]; then
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -f rocpd csv -d $OUT/all/trace -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
+        find $OUT/all/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+        continue
+    fi
     B="--legs $G --steps 3 --warmup 1 --no-cpu-baseline --pipeline 1 --pairing-pipeline 1"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -f rocpd csv -d $OUT/$G/trace -o run -- python3 bench.py $B > $OUT/$G.trace.log 2>&1 || { echo "trace pass $G failed"; exit 1; }
     find $OUT/$G/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_$G.csv \;
