@@ -928,6 +928,144 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
     if (!role) fp12_store(fv, nlanes, c, f);
 }
 
+// ---- two-lane line precomputation, for batches too small to give every SIMD a wave: lanes (2j, 2j+1)
+// compute pair j's 91 lines together.  Both lanes hold the twist point R and the pair; each step's
+// F_p^2 products are split into levels of two independent products, one per lane (the operands are
+// selected by the lane's role, not branched on), and the results swapped between the two lanes with a
+// DPP quad permutation (no LDS round trip), so the dependent chain per step is about half as long.
+// Every value is the same field element as line_double_i / line_add_i compute (optate.go:3-92).
+GSV_DI uint32_t dpp_swap(uint32_t v) {  // the partner lane's v (lanes 2k <-> 2k+1)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1 /* quad_perm [1,0,3,2] */, 0xF, 0xF, false);
+}
+template <class T>
+GSV_DI T xch2(const T& mine) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized");
+    T o;
+    const uint32_t* m = (const uint32_t*)&mine;
+    uint32_t* w = (uint32_t*)&o;
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); k++) w[k] = dpp_swap(m[k]);
+    return o;
+}
+// (mine, partner's) ordered by role: first = role 0's value
+GSV_DI void split2(fp2& r0, fp2& r1, const fp2& mine, bool role) {
+    fp2 other = xch2(mine);
+    r0 = role ? other : mine;
+    r1 = role ? mine : other;
+}
+
+GSV_DI fq selq(bool r, const fq& a, const fq& b) {  // r ? b : a
+    fq o;
+#pragma unroll
+    for (int k = 0; k < 9; k++) o.v[k] = r ? b.v[k] : a.v[k];
+    return o;
+}
+// Each level is ONE operation of one kind (a squaring, or a product) on operands selected by role: the
+// wave executes it once for both lanes (a ternary over two different operations would run both).
+// optate.go:52-92: 8 S + 3 M + 2 (F_p^2 x F_p) in one lane's chain -> 5 S + 2 M + 1 (x F_p) here
+GSV_DI line line_double2(g2j& r, const g1a& q, bool role) {
+    fp2 A, B, C, S, G, Tz, U, V, W, Xz, lb, lc;
+    split2(A, B, s2(fp2_sqr(role ? r.y : r.x)), role);                    // A = x^2 | B = y^2
+    split2(C, S, s2(fp2_sqr(sel2(role, B, fp2_add(r.x, B)))), role);      // C = B^2 | S = (x + B)^2
+    fp2 D = s2(fp2_dbl(fp2_sub(fp2_sub(S, A), C)));
+    fp2 E = s2(fp2_add(fp2_dbl(A), A));
+    split2(G, Tz, s2(fp2_sqr(sel2(role, E, fp2_add(r.y, r.z)))), role);   // G = E^2 | (y + z)^2
+    g2j o;
+    o.z = s2(fp2_sub(fp2_sub(Tz, B), r.t));
+    o.x = s2(fp2_sub(G, fp2_dbl(D)));
+    fp2 xe = s2(fp2_add(r.x, E));
+    split2(U, V, s2(fp2_mul(role ? E : xe, role ? r.t : xe)), role);      // U = (x + E)^2 | V = E t
+    split2(W, Xz, s2(fp2_mul(sel2(role, fp2_sub(D, o.x), o.z), role ? r.t : E)), role);  // (D - o.x) E | o.z t
+    o.y = s2(fp2_sub(W, fp2_mul_small<8>(C)));
+    o.t = s2(fp2_sqr(o.z));
+    split2(lb, lc, s2(fp2_mul_fp(role ? s2(fp2_dbl(Xz)) : s2(fp2_neg(fp2_dbl(V))), selq(role, q.x, q.y))), role);
+    line l;
+    l.a = s2(fp2_sub(fp2_sub(fp2_sub(U, A), G), fp2_mul_small<4>(B)));
+    l.b = lb;
+    l.c = lc;
+    r = o;
+    return l;
+}
+// optate.go:3-50 (mixed addition r + p, p affine with t = 1; r2 = p.y^2):
+// 6 S + 8 M + 2 (x F_p) in one lane's chain -> 2 S + 5 M + 1 (x F_p) here
+GSV_DI line line_add2(g2j& r, const g2a& p, const g1a& q, const fp2& r2, bool role) {
+    fp2 B, K, D, I, J, V, Lsq, Tz, W, Y, Pz, ot, M, lc;
+    fp2 yz = s2(fp2_add(p.y, r.z));
+    split2(B, K, s2(fp2_mul(role ? yz : p.x, role ? yz : r.t)), role);   // B = p.x t | (p.y + z)^2
+    fp2 H = s2(fp2_sub(B, r.x));
+    fp2 kk = s2(fp2_sub(fp2_sub(K, r2), r.t));
+    split2(D, I, s2(fp2_mul(role ? H : kk, role ? H : r.t)), role);      // D = (K - r2 - t) t | I = H^2
+    fp2 E = s2(fp2_mul_small<4>(I));
+    fp2 L1 = s2(fp2_sub(D, fp2_dbl(r.y)));
+    split2(J, V, s2(fp2_mul(role ? r.x : H, E)), role);                  // J = H E | V = x E
+    split2(Lsq, Tz, s2(fp2_sqr(sel2(role, L1, fp2_add(r.z, H)))), role);  // L1^2 | (z + H)^2
+    g2j o;
+    o.x = s2(fp2_sub(fp2_sub(Lsq, J), fp2_dbl(V)));
+    o.z = s2(fp2_sub(fp2_sub(Tz, r.t), I));
+    split2(W, Y, s2(fp2_mul(sel2(role, fp2_sub(V, o.x), r.y), role ? J : L1)), role);  // (V - o.x) L1 | y J
+    o.y = s2(fp2_sub(W, fp2_dbl(Y)));
+    split2(ot, Pz, s2(fp2_sqr(sel2(role, o.z, fp2_add(p.y, o.z)))), role);  // o.t = o.z^2 | (p.y + o.z)^2
+    o.t = ot;
+    {  // M = L1 p.x | l.c = 2 o.z (P.y, 0)
+        fp2 py0{fq_zero(), q.y};  // P.y as an F_p^2 element (x i + y: imaginary part 0)
+        split2(M, lc, s2(fp2_mul(role ? s2(fp2_dbl(o.z)) : L1, role ? py0 : p.x)), role);
+    }
+    line l;
+    l.a = s2(fp2_sub(fp2_dbl(M), fp2_sub(fp2_sub(Pz, r2), o.t)));
+    l.c = lc;
+    l.b = s2(fp2_mul_fp(fp2_dbl(fp2_neg(L1)), q.x));
+    r = o;
+    return l;
+}
+// the pair's lines, role 0 storing a and b, role 1 c
+GSV_DI void line_store2(uint32_t* __restrict__ lines, uint32_t n, uint32_t j, int li, const line& l, bool role) {
+    if (!role) {
+        soa_store2(lines, n, j, li * 6 + 0, l.a);
+        soa_store2(lines, n, j, li * 6 + 2, l.b);
+    } else {
+        soa_store2(lines, n, j, li * 6 + 4, l.c);
+    }
+}
+GSV_DI void pair_lines2(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j, const g1a& P, const g2a& Q, bool role) {
+    g2j r{Q.x, Q.y, fp2_one(), fp2_one()};
+    int li = 0;
+#pragma unroll 1
+    for (int i = 64; i > 0; i--) {
+        line_store2(lines, npairs, j, li++, line_double2(r, P, role), role);
+        uint64_t bit = 1ull << (i - 1);
+        if ((NAF_POS | NAF_NEG) & bit) {
+            g2a qq{Q.x, (NAF_POS & bit) ? Q.y : s2(fp2_neg(Q.y))};
+            line_store2(lines, npairs, j, li++, line_add2(r, qq, P, s2(fp2_sqr(Q.y)), role), role);
+        }
+    }
+    g2a q1{s2(fp2_mul(fp2_conj(Q.x), fp2_const(FQ_XI_P1_3_X, FQ_XI_P1_3_Y))),
+           s2(fp2_mul(fp2_conj(Q.y), fp2_const(FQ_XI_P1_2_X, FQ_XI_P1_2_Y)))};
+    g2a mq2{s2(fp2_mul_fp(Q.x, fq_const(FQ_XI_PSQ1_3))), Q.y};
+    line_store2(lines, npairs, j, li++, line_add2(r, q1, P, s2(fp2_sqr(q1.y)), role), role);
+    line_store2(lines, npairs, j, li, line_add2(r, mq2, P, s2(fp2_sqr(mq2.y)), role), role);
+}
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_LINES_WAVES))) void k_bn_lines2(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ pair_src, uint32_t npairs, uint32_t* __restrict__ lines,
+    uint8_t* __restrict__ luse) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t j = t >> 1;
+    bool role = (t & 1u) != 0;
+    if (j >= npairs) return;  // both lanes of a pair leave together
+    const uint8_t* s = in + pair_src[j];
+    g1a P;
+    g2a Q;
+    bool ok = fp_unmarshal(P.x, s);
+    ok = fp_unmarshal(P.y, s + 32) && ok;
+    ok = fp_unmarshal(Q.x.x, s + 64) && ok;
+    ok = fp_unmarshal(Q.x.y, s + 96) && ok;
+    ok = fp_unmarshal(Q.y.x, s + 128) && ok;
+    ok = fp_unmarshal(Q.y.y, s + 160) && ok;
+    bool inf1 = fq_is_zero(P.x) && fq_is_zero(P.y);
+    bool inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
+    if (!role) luse[j] = ok && !inf1 && !inf2 ? PS_OK : PS_SKIP;
+    pair_lines2(lines, npairs, j, P, Q, role);
+}
+
 // role/base as final_exp: the verdict is written by role 0
 // cbad[c] != 0: the check's input length is not a multiple of 192 (errBadPairingInput,
 // core/vm/contracts.go:336-338); it has no pairs
@@ -1165,8 +1303,12 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                            d_pstat);
         if (hipEventRecord(conc->join, conc->side) != hipSuccess) return hipErrorUnknown;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                           d_lines, conc->d_luse);
+        if (layout & GSV_BN_LAYOUT_LINES2)
+            hipLaunchKernelGGL(bn::k_bn_lines2, dim3((2 * npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src,
+                               npairs, d_lines, conc->d_luse);
+        else
+            hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
+                               d_lines, conc->d_luse);
         if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
