@@ -354,6 +354,7 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
             "traffic": pmc_traffic(k),
             "traffic_source": f"profiles/{ROUND}/pmc_ecrecover.json" if pmc_traffic(k) else None,
             "profiled_kernel_avg_ms": k.get("avg_ms"),
+            "trace_agreement": f"profiles/{ROUND}/trace_agreement.json",
             "algorithmic_bytes_per_launch": N_SIGS * (32 + 65 + 65 + 20 + 1),
             # by design: one 80-byte affine comb entry per 20-bit window of u1 (13 per recovery) from the
             # 1.09 GB table in HBM (gsv_internal.h GSV_COMB_BITS)
@@ -434,7 +435,8 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
             "hbm_GBps": round(traffic / (k["avg_ms"] * 1e-3) / 1e9, 1) if traffic and k.get("avg_ms") else None,
             "hbm_frac": round(traffic / (k["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
             if traffic and k.get("avg_ms") else None,
-            "permutations_per_launch": bot_perms}
+            "permutations_per_launch": bot_perms, "profiled_kernel_avg_ms": k.get("avg_ms"),
+            "trace_agreement": f"profiles/{ROUND}/trace_agreement.json"}
     out = {"collation_GBps": round(ws * N_SHARDS * BODY * csteps / cdt / 1e9, 3),
            "shards": N_SHARDS * ws, "body_bytes": BODY, "ms_per_step": round(cdt / csteps * 1e3, 3),
            "pipeline_depth": depth,
@@ -613,7 +615,7 @@ def leg_keccak(ctx, stream, dev, ws, rank, args):
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
             "traffic": traffic, "algorithmic_bytes_per_launch": int(voff[-1]) + (nblk * ntx + 1) * 8 + nblk * ntx * 32,
             "hbm_GBps": round(traffic / (k["avg_ms"] * 1e-3) / 1e9, 1) if traffic and k.get("avg_ms") else None,
-            "permutations_per_launch": perms}
+            "permutations_per_launch": perms, "profiled_kernel_avg_ms": k.get("avg_ms")}
     return {"hashes_per_s": round(ws * nblk * ntx * ksteps / kdt, 1),
             "GBps": round(ws * float(voff[-1]) * ksteps / kdt / 1e9, 3),
             "permutations_per_s": round(ws * perms * ksteps / kdt, 1),
