@@ -928,9 +928,10 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.stage(s.o_cbad, bad_len.data(), n);
     return GSV_SUCCESS;
 }
-// the concurrent layout's side streams and events, one set per instance (at prepare / host-path build)
-int pairing_conc_init(Shape& s) {
-    if (!(s.layout & gsv::GSV_BN_LAYOUT_CONC) || !s.side.empty()) return GSV_SUCCESS;
+// a side stream and fork/join events per instance (at prepare / host-path build), for shapes that run
+// two independent launch chains at once: the pairing's concurrent layout, the notary's chunk roots
+int shape_side_init(Shape& s) {
+    if (!s.side.empty()) return GSV_SUCCESS;
     s.side.assign(s.ninst, nullptr);
     s.efork.assign(s.ninst, nullptr);
     s.ejoin.assign(s.ninst, nullptr);
@@ -940,6 +941,10 @@ int pairing_conc_init(Shape& s) {
         HIPCHK(hipEventCreateWithFlags(&s.ejoin[k], hipEventDisableTiming));
     }
     return GSV_SUCCESS;
+}
+int pairing_conc_init(Shape& s) {
+    if (!(s.layout & gsv::GSV_BN_LAYOUT_CONC)) return GSV_SUCCESS;
+    return shape_side_init(s);
 }
 int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verdict, hipStream_t st) {
     gsv::BnConcurrent conc{};
@@ -957,6 +962,9 @@ int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verd
 }
 
 // ---- notary: key = chain id, signer, max_txs, body offsets
+#ifndef GSV_NOTARY_FORK
+#define GSV_NOTARY_FORK 1
+#endif
 std::vector<uint64_t> notary_key(const uint64_t* h_off, size_t n, const uint8_t* cid, size_t cidlen, int signer,
                                  uint32_t max_txs) {
     std::vector<uint64_t> k{(uint64_t)signer, max_txs};
@@ -1010,6 +1018,20 @@ int notary_run(gsv_ctx* c, const Shape& s, size_t n, const uint8_t* d_bodies, ui
     uint32_t* d_cnt = d_ntx ? d_ntx : s.at<uint32_t>(s.o_cnt);
     if (d_senders) HIPCHK(hipMemsetAsync(d_senders, 0, n * s.max_txs * 20, st));
     if (d_status) HIPCHK(hipMemsetAsync(d_status, GSV_ST_BAD_RLP, n * s.max_txs, st));
+    // The chunk roots of the same bodies are independent of the transactions: with a side stream they
+    // run beside the blob decode + recovery (fork / join by events, so a capture still works) and
+    // fill the SIMDs the recovery kernel's tail and the trie top leave idle.
+    const bool fork = GSV_NOTARY_FORK && (size_t)s.cur < s.side.size();
+    if (fork) {
+        HIPCHK(hipEventRecord(s.efork[s.cur], st));
+        HIPCHK(hipStreamWaitEvent(s.side[s.cur], s.efork[s.cur], 0));
+        hipStream_t keep = c->cur_stream;
+        c->cur_stream = s.side[s.cur];  // the chunk-root launch hooks time on the stream they run on
+        int rc = chunk_run(c, s, s.chunk, d_bodies, d_root, s.side[s.cur]);
+        c->cur_stream = keep;
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(s.ejoin[s.cur], s.side[s.cur]));
+    }
     hook_begin(c, GSV_K_NOTARY);
     HIPCHK(gsv::launch_blob_index(d_bodies, s.at<uint64_t>(s.o_noff), s.at<uint32_t>(s.o_nlen), (uint32_t)n,
                                   s.max_txs, s.at<void>(s.o_blobs), d_cnt, st));
@@ -1017,6 +1039,10 @@ int notary_run(gsv_ctx* c, const Shape& s, size_t n, const uint8_t* d_bodies, ui
                                  s.max_txs, s.at<uint8_t>(s.o_cid), s.at<uint8_t>(s.o_cid) + 64, s.sfx_len,
                                  s.signer_kind, c->gtab, d_bitmap, (uint32_t)bm, d_senders, d_status, st));
     hook_end(c, GSV_K_NOTARY);
+    if (fork) {
+        HIPCHK(hipStreamWaitEvent(st, s.ejoin[s.cur], 0));
+        return GSV_SUCCESS;
+    }
     return chunk_run(c, s, s.chunk, d_bodies, d_root, st);  // chunk roots of the same bodies
 }
 
@@ -1495,12 +1521,14 @@ int gsv_notary_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n_shards, const
     std::lock_guard<std::mutex> g(c->smu);
     HIPCHK(hipSetDevice(c->device));
     Shape* s;
-    return shape_get(c, SK_NOTARY, notary_key(h_off, n_shards, chain_id, chain_id_len, signer_kind, max_txs),
-                     [&](Shape& ns, Layout& L) {
-                         return notary_shape(c, ns, h_off, h_off + 1, n_shards, chain_id, chain_id_len, signer_kind,
-                                             max_txs, L);
-                     },
-                     &s);
+    rc = shape_get(c, SK_NOTARY, notary_key(h_off, n_shards, chain_id, chain_id_len, signer_kind, max_txs),
+                   [&](Shape& ns, Layout& L) {
+                       return notary_shape(c, ns, h_off, h_off + 1, n_shards, chain_id, chain_id_len, signer_kind,
+                                           max_txs, L);
+                   },
+                   &s);
+    if (rc) return rc;
+    return shape_side_init(*s);
 }
 
 int gsv_notary_validate_shards_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n_shards,
@@ -1543,6 +1571,8 @@ int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t
                                             signer_kind, max_txs, L);
                     },
                     s);
+    if (rc) return rc;
+    rc = shape_side_init(s);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_b = cv.take<uint8_t>(pos + 16);
@@ -1632,13 +1662,15 @@ int gsv_notary_partition_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n_tot
     std::lock_guard<std::mutex> g(c->smu);
     HIPCHK(hipSetDevice(c->device));
     Shape* s;
-    return shape_get(c, SK_PARTITION,
-                     partition_key(h_off, d.n, n_total, nranks, rank, chain_id, chain_id_len, signer_kind, max_txs),
-                     [&](Shape& ns, Layout& L) {
-                         return partition_shape(c, ns, h_off, n_total, nranks, rank, chain_id, chain_id_len,
-                                                signer_kind, max_txs, L);
-                     },
-                     &s);
+    rc = shape_get(c, SK_PARTITION,
+                   partition_key(h_off, d.n, n_total, nranks, rank, chain_id, chain_id_len, signer_kind, max_txs),
+                   [&](Shape& ns, Layout& L) {
+                       return partition_shape(c, ns, h_off, n_total, nranks, rank, chain_id, chain_id_len,
+                                              signer_kind, max_txs, L);
+                   },
+                   &s);
+    if (rc) return rc;
+    return d.n ? shape_side_init(*s) : GSV_SUCCESS;
 }
 
 int gsv_notary_partition_pack_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n_total,
@@ -1762,6 +1794,7 @@ int gsv_notary_validate_partition(gsv_ctx* c, const uint8_t* bodies, const uint6
                                                  max_txs, L);
                          },
                          s);
+        if (!lrc && n) lrc = shape_side_init(s);
     }
     if (lrc && arena_reserve(c, out_bytes)) return lrc;  // cannot even join the collective
     Carve cv(c->arena);
