@@ -374,11 +374,14 @@ GSV_DI g2j g2_psi(const g2j& a) {
     o.t = a.t;
     return o;
 }
-// twist.go:47-63: y^2 == x^3 + 3/xi and Q in the order-r subgroup
+// twist.go:47-58: y^2 == x^3 + 3/xi
+GSV_DI bool g2_on_twist(const g2a& q) {
+    return fp2_eq(fp2_sqr(q.y), fp2_add(fp2_mul(fp2_sqr(q.x), q.x), fp2_const(FQ_TWIST_B_X, FQ_TWIST_B_Y)));
+}
+// twist.go:47-63: y^2 == x^3 + 3/xi and Q in the order-r subgroup (the BN_SUB_FROB = 0 build)
 static BN_NI bool g2_in_subgroup(const g2a* pq) {
     const g2a q = *pq;
-    if (!fp2_eq(fp2_sqr(q.y), fp2_add(fp2_mul(fp2_sqr(q.x), q.x), fp2_const(FQ_TWIST_B_X, FQ_TWIST_B_Y))))
-        return false;
+    if (!g2_on_twist(q)) return false;
     // The reference decides membership with Order*Q == infinity (twist.go:60-62, 254-bit
     // double-and-add).  We decide the same predicate with the endomorphism psi (the
     // untwist-Frobenius-twist map the Miller loop already uses for Q1, optate.go:173-176):
@@ -404,6 +407,31 @@ static BN_NI bool g2_in_subgroup(const g2a* pq) {
     rhs.y = s2(fp2_neg(rhs.y));
     g2j d = g2_add_i(lhs, rhs);                          // lhs - rhs
     return fp2_is_zero(d.z);
+}
+
+// Subgroup membership from the line chain's own final point (BN_SUB_FROB).  The lines of a pair leave
+// r = [6u+2]Q + psi(Q) - psi^2(Q) (optate.go:122-210: the NAF doublings / additions, then the two
+// Frobenius additions), and for every Q on E'(F_p^2) of BN254
+//     [r]Q == O (twist.go:60-62)   <=>   r + psi^3(Q) == O.
+// On G2, psi acts as [p] and 6u+2 + p - p^2 + p^3 == 0 mod r (the optimal-ate relation).  E'(F_p^2)
+// = G2 x H with #H = h = 2p - r coprime to r; psi satisfies psi^2 - t psi + p = 0, so
+// f(psi) = 6u+2 + psi - psi^2 + psi^3 = a + b psi with a = p + 6u+2 - tp, b = t^2 - t - p + 1, and
+// (a + b psi~)(a + b psi) = a^2 + abt + b^2 p is coprime to h: f(psi) is injective on H, so
+// r + psi^3(Q) == O only for Q in G2 (tests/test_g2_frob_relation.py checks these numbers and the
+// relation on random points in G2, in H and in neither).  The chain's formulas meet an exceptional
+// case (r == +-q at an addition, a 2-torsion r at a doubling) only when they output Z = 0, which every
+// later step keeps at 0; that reads as "not in G2", and for Q in G2 no multiple the chain meets is
+// +-Q (6u+2 -+ p, 6u+2 + p -+ p^2 are nonzero mod r), so members never get there.  It replaces the
+// separate 63-bit psi test: no second G2 chain per pair.
+GSV_DI bool g2_frob_check(const g2j& r, const g2a& Q) {
+    fp2 x = Q.x, y = Q.y;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {  // psi^3(Q) = (x', y'); r == -psi^3(Q) <=> Z != 0, X == x' Z^2, Y == -y' Z^3
+        x = s2(fp2_mul(fp2_conj(x), fp2_const(FQ_XI_P1_3_X, FQ_XI_P1_3_Y)));
+        y = s2(fp2_mul(fp2_conj(y), fp2_const(FQ_XI_P1_2_X, FQ_XI_P1_2_Y)));
+    }
+    fp2 z2 = s2(fp2_sqr(r.z));
+    return !fp2_is_zero(r.z) && fp2_eq(r.x, fp2_mul(x, z2)) && fp2_eq(fp2_neg(r.y), fp2_mul(y, fp2_mul(z2, r.z)));
 }
 
 // ---------------------------------------------------------------- Miller loop (optate.go)
@@ -612,7 +640,7 @@ enum : uint8_t { PS_OK = 0, PS_SKIP = 1, PS_BAD = 2 };
 // The lines of one pair (optate.go:122-210 for affine Q and P, neither at infinity: the loop's
 // doubling / addition steps and the two Frobenius additions), in the order the Miller loop
 // multiplies them in.  Lines of an invalid or infinite pair are computed but never used.
-GSV_DI void pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j, const g1a& P, const g2a& Q) {
+GSV_DI g2j pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j, const g1a& P, const g2a& Q) {
     g2j r{Q.x, Q.y, fp2_one(), fp2_one()};
     int li = 0;
 #if BN_LINES_LEAN
@@ -643,8 +671,14 @@ GSV_DI void pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j
     g2a mq2{s2(fp2_mul_fp(Q.x, fq_const(FQ_XI_PSQ1_3))), Q.y};
     line_store(lines, npairs, j, li++, line_add_i(r, q1, P, s2(fp2_sqr(q1.y))));
     line_store(lines, npairs, j, li, line_add_i(r, mq2, P, s2(fp2_sqr(mq2.y))));
+    return r;
 }
 
+// 1: subgroup membership from the line chain (g2_frob_check), one lane per pair; 0: the separate check
+// role with the 63-bit psi test (A/B)
+#ifndef BN_SUB_FROB
+#define BN_SUB_FROB 1
+#endif
 // role 0 (checks) / role 1 (lines) of pair i.  With `luse` (the concurrent layout) the lines role also
 // writes whether the Miller loop uses the pair's lines: PS_OK for a decoded pair with neither point at
 // infinity, PS_SKIP otherwise; the curve / subgroup verdict (pstat) then arrives only for k_bn_final.
@@ -662,6 +696,18 @@ GSV_DI void prepare_pair(bool role_lines, uint32_t i, const uint8_t* __restrict_
     ok = fp_unmarshal(Q.y.y, s + 160) && ok;
     bool inf1 = fq_is_zero(P.x) && fq_is_zero(P.y);
     bool inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
+#if BN_SUB_FROB
+    // one lane does the whole pair: curve checks, lines, and membership from the lines' final point
+    (void)role_lines;
+    (void)luse;
+    if (ok && !inf1)  // curve.go:39-52: y^2 == x^3 + 3
+        ok = fq_eq(fq_mul(P.y, P.y), fq_add(fq_mul(fq_mul(P.x, P.x), P.x), fq_const(FQ_THREE)));
+    if (ok && !inf2) ok = g2_on_twist(Q);
+    g2j r = pair_lines(lines, npairs, i, P, Q);
+    if (ok && !inf2) ok = g2_frob_check(r, Q);
+    pstat[i] = !ok ? PS_BAD : (inf1 || inf2) ? PS_SKIP : PS_OK;
+    return;
+#endif
     if (role_lines) {
         if (luse) luse[i] = ok && !inf1 && !inf2 ? PS_OK : PS_SKIP;
         pair_lines(lines, npairs, i, P, Q);
@@ -685,11 +731,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVE
                                                    const uint64_t* __restrict__ pair_src,
                                                    uint32_t npairs, uint8_t* __restrict__ pstat,
                                                    uint32_t* __restrict__ lines /* [91 * 54 words][npairs] */) {
+#if BN_SUB_FROB
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // one role: grid of (npairs + 63) / 64 blocks
+    if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, pstat, lines);
+#else
     uint32_t nb = (npairs + 63) / 64;
     bool role_lines = blockIdx.x >= nb;
     uint32_t i = (role_lines ? blockIdx.x - nb : blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= npairs) return;
     prepare_pair(role_lines, i, in, pair_src, npairs, pstat, lines);
+#endif
 }
 // BN_PREP_SPLIT: the two roles as separate kernels, each with its own register budget (A/B)
 #ifndef BN_PREP_SPLIT
@@ -698,18 +749,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVE
 #ifndef BN_LINES_WAVES
 #define BN_LINES_WAVES 1
 #endif
+#if !BN_SUB_FROB
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVES))) void k_bn_check(const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ pair_src,
                                                    uint32_t npairs, uint8_t* __restrict__ pstat) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < npairs) prepare_pair(false, i, in, pair_src, npairs, pstat, nullptr);
 }
+#endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_LINES_WAVES))) void k_bn_lines(const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ pair_src,
                                                    uint32_t npairs, uint32_t* __restrict__ lines,
-                                                   uint8_t* __restrict__ luse) {
+                                                   uint8_t* __restrict__ luse, uint8_t* __restrict__ pstat) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, nullptr, lines, luse);
+    if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, pstat, lines, luse);
 }
 
 // ---- per-check multi-Miller loop.  The product of a check's Miller values equals one loop that
@@ -926,144 +979,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
         for (int k = 0; k < 2; k++) mul_line2(f, line_load(lines, npairs, j, li + k), role, base);
     }
     if (!role) fp12_store(fv, nlanes, c, f);
-}
-
-// ---- two-lane line precomputation, for batches too small to give every SIMD a wave: lanes (2j, 2j+1)
-// compute pair j's 91 lines together.  Both lanes hold the twist point R and the pair; each step's
-// F_p^2 products are split into levels of two independent products, one per lane (the operands are
-// selected by the lane's role, not branched on), and the results swapped between the two lanes with a
-// DPP quad permutation (no LDS round trip), so the dependent chain per step is about half as long.
-// Every value is the same field element as line_double_i / line_add_i compute (optate.go:3-92).
-GSV_DI uint32_t dpp_swap(uint32_t v) {  // the partner lane's v (lanes 2k <-> 2k+1)
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1 /* quad_perm [1,0,3,2] */, 0xF, 0xF, false);
-}
-template <class T>
-GSV_DI T xch2(const T& mine) {
-    static_assert(sizeof(T) % 4 == 0, "word-sized");
-    T o;
-    const uint32_t* m = (const uint32_t*)&mine;
-    uint32_t* w = (uint32_t*)&o;
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(T) / 4); k++) w[k] = dpp_swap(m[k]);
-    return o;
-}
-// (mine, partner's) ordered by role: first = role 0's value
-GSV_DI void split2(fp2& r0, fp2& r1, const fp2& mine, bool role) {
-    fp2 other = xch2(mine);
-    r0 = role ? other : mine;
-    r1 = role ? mine : other;
-}
-
-GSV_DI fq selq(bool r, const fq& a, const fq& b) {  // r ? b : a
-    fq o;
-#pragma unroll
-    for (int k = 0; k < 9; k++) o.v[k] = r ? b.v[k] : a.v[k];
-    return o;
-}
-// Each level is ONE operation of one kind (a squaring, or a product) on operands selected by role: the
-// wave executes it once for both lanes (a ternary over two different operations would run both).
-// optate.go:52-92: 8 S + 3 M + 2 (F_p^2 x F_p) in one lane's chain -> 5 S + 2 M + 1 (x F_p) here
-GSV_DI line line_double2(g2j& r, const g1a& q, bool role) {
-    fp2 A, B, C, S, G, Tz, U, V, W, Xz, lb, lc;
-    split2(A, B, s2(fp2_sqr(role ? r.y : r.x)), role);                    // A = x^2 | B = y^2
-    split2(C, S, s2(fp2_sqr(sel2(role, B, fp2_add(r.x, B)))), role);      // C = B^2 | S = (x + B)^2
-    fp2 D = s2(fp2_dbl(fp2_sub(fp2_sub(S, A), C)));
-    fp2 E = s2(fp2_add(fp2_dbl(A), A));
-    split2(G, Tz, s2(fp2_sqr(sel2(role, E, fp2_add(r.y, r.z)))), role);   // G = E^2 | (y + z)^2
-    g2j o;
-    o.z = s2(fp2_sub(fp2_sub(Tz, B), r.t));
-    o.x = s2(fp2_sub(G, fp2_dbl(D)));
-    fp2 xe = s2(fp2_add(r.x, E));
-    split2(U, V, s2(fp2_mul(role ? E : xe, role ? r.t : xe)), role);      // U = (x + E)^2 | V = E t
-    split2(W, Xz, s2(fp2_mul(sel2(role, fp2_sub(D, o.x), o.z), role ? r.t : E)), role);  // (D - o.x) E | o.z t
-    o.y = s2(fp2_sub(W, fp2_mul_small<8>(C)));
-    o.t = s2(fp2_sqr(o.z));
-    split2(lb, lc, s2(fp2_mul_fp(role ? s2(fp2_dbl(Xz)) : s2(fp2_neg(fp2_dbl(V))), selq(role, q.x, q.y))), role);
-    line l;
-    l.a = s2(fp2_sub(fp2_sub(fp2_sub(U, A), G), fp2_mul_small<4>(B)));
-    l.b = lb;
-    l.c = lc;
-    r = o;
-    return l;
-}
-// optate.go:3-50 (mixed addition r + p, p affine with t = 1; r2 = p.y^2):
-// 6 S + 8 M + 2 (x F_p) in one lane's chain -> 2 S + 5 M + 1 (x F_p) here
-GSV_DI line line_add2(g2j& r, const g2a& p, const g1a& q, const fp2& r2, bool role) {
-    fp2 B, K, D, I, J, V, Lsq, Tz, W, Y, Pz, ot, M, lc;
-    fp2 yz = s2(fp2_add(p.y, r.z));
-    split2(B, K, s2(fp2_mul(role ? yz : p.x, role ? yz : r.t)), role);   // B = p.x t | (p.y + z)^2
-    fp2 H = s2(fp2_sub(B, r.x));
-    fp2 kk = s2(fp2_sub(fp2_sub(K, r2), r.t));
-    split2(D, I, s2(fp2_mul(role ? H : kk, role ? H : r.t)), role);      // D = (K - r2 - t) t | I = H^2
-    fp2 E = s2(fp2_mul_small<4>(I));
-    fp2 L1 = s2(fp2_sub(D, fp2_dbl(r.y)));
-    split2(J, V, s2(fp2_mul(role ? r.x : H, E)), role);                  // J = H E | V = x E
-    split2(Lsq, Tz, s2(fp2_sqr(sel2(role, L1, fp2_add(r.z, H)))), role);  // L1^2 | (z + H)^2
-    g2j o;
-    o.x = s2(fp2_sub(fp2_sub(Lsq, J), fp2_dbl(V)));
-    o.z = s2(fp2_sub(fp2_sub(Tz, r.t), I));
-    split2(W, Y, s2(fp2_mul(sel2(role, fp2_sub(V, o.x), r.y), role ? J : L1)), role);  // (V - o.x) L1 | y J
-    o.y = s2(fp2_sub(W, fp2_dbl(Y)));
-    split2(ot, Pz, s2(fp2_sqr(sel2(role, o.z, fp2_add(p.y, o.z)))), role);  // o.t = o.z^2 | (p.y + o.z)^2
-    o.t = ot;
-    {  // M = L1 p.x | l.c = 2 o.z (P.y, 0)
-        fp2 py0{fq_zero(), q.y};  // P.y as an F_p^2 element (x i + y: imaginary part 0)
-        split2(M, lc, s2(fp2_mul(role ? s2(fp2_dbl(o.z)) : L1, role ? py0 : p.x)), role);
-    }
-    line l;
-    l.a = s2(fp2_sub(fp2_dbl(M), fp2_sub(fp2_sub(Pz, r2), o.t)));
-    l.c = lc;
-    l.b = s2(fp2_mul_fp(fp2_dbl(fp2_neg(L1)), q.x));
-    r = o;
-    return l;
-}
-// the pair's lines, role 0 storing a and b, role 1 c
-GSV_DI void line_store2(uint32_t* __restrict__ lines, uint32_t n, uint32_t j, int li, const line& l, bool role) {
-    if (!role) {
-        soa_store2(lines, n, j, li * 6 + 0, l.a);
-        soa_store2(lines, n, j, li * 6 + 2, l.b);
-    } else {
-        soa_store2(lines, n, j, li * 6 + 4, l.c);
-    }
-}
-GSV_DI void pair_lines2(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j, const g1a& P, const g2a& Q, bool role) {
-    g2j r{Q.x, Q.y, fp2_one(), fp2_one()};
-    int li = 0;
-#pragma unroll 1
-    for (int i = 64; i > 0; i--) {
-        line_store2(lines, npairs, j, li++, line_double2(r, P, role), role);
-        uint64_t bit = 1ull << (i - 1);
-        if ((NAF_POS | NAF_NEG) & bit) {
-            g2a qq{Q.x, (NAF_POS & bit) ? Q.y : s2(fp2_neg(Q.y))};
-            line_store2(lines, npairs, j, li++, line_add2(r, qq, P, s2(fp2_sqr(Q.y)), role), role);
-        }
-    }
-    g2a q1{s2(fp2_mul(fp2_conj(Q.x), fp2_const(FQ_XI_P1_3_X, FQ_XI_P1_3_Y))),
-           s2(fp2_mul(fp2_conj(Q.y), fp2_const(FQ_XI_P1_2_X, FQ_XI_P1_2_Y)))};
-    g2a mq2{s2(fp2_mul_fp(Q.x, fq_const(FQ_XI_PSQ1_3))), Q.y};
-    line_store2(lines, npairs, j, li++, line_add2(r, q1, P, s2(fp2_sqr(q1.y)), role), role);
-    line_store2(lines, npairs, j, li, line_add2(r, mq2, P, s2(fp2_sqr(mq2.y)), role), role);
-}
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_LINES_WAVES))) void k_bn_lines2(
-    const uint8_t* __restrict__ in, const uint64_t* __restrict__ pair_src, uint32_t npairs, uint32_t* __restrict__ lines,
-    uint8_t* __restrict__ luse) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t j = t >> 1;
-    bool role = (t & 1u) != 0;
-    if (j >= npairs) return;  // both lanes of a pair leave together
-    const uint8_t* s = in + pair_src[j];
-    g1a P;
-    g2a Q;
-    bool ok = fp_unmarshal(P.x, s);
-    ok = fp_unmarshal(P.y, s + 32) && ok;
-    ok = fp_unmarshal(Q.x.x, s + 64) && ok;
-    ok = fp_unmarshal(Q.x.y, s + 96) && ok;
-    ok = fp_unmarshal(Q.y.x, s + 128) && ok;
-    ok = fp_unmarshal(Q.y.y, s + 160) && ok;
-    bool inf1 = fq_is_zero(P.x) && fq_is_zero(P.y);
-    bool inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
-    if (!role) luse[j] = ok && !inf1 && !inf2 ? PS_OK : PS_SKIP;
-    pair_lines2(lines, npairs, j, P, Q, role);
 }
 
 // role/base as final_exp: the verdict is written by role 0
@@ -1293,32 +1208,45 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
     // loop (on the lines role's PS_OK / PS_SKIP) and join before the final exponentiation, which reads
     // their verdicts; the lines kernel has a one-wave register budget (no spills).  For batches that
     // leave SIMDs idle: the check waves fill them.
-    const bool cc = (layout & GSV_BN_LAYOUT_CONC) && conc && npairs;
+    // BN_SUB_FROB: no check role (membership comes from the lines), so GSV_BN_LAYOUT_CONC only selects
+    // the one-wave-budget lines kernel; nothing forks.
+    const bool cc = !BN_SUB_FROB && (layout & GSV_BN_LAYOUT_CONC) && conc && npairs;
     bn::PairBad pb{d_lane_first, d_pidx, cc ? d_pstat : nullptr};
     const uint8_t* d_use = cc ? conc->d_luse : d_pstat;
-    if (cc) {
+    if (BN_SUB_FROB && npairs) {
+        if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
+        if (layout & GSV_BN_LAYOUT_CONC)
+            hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
+                               d_lines, (uint8_t*)nullptr, d_pstat);
+        else
+            hipLaunchKernelGGL(bn::k_bn_prepare, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
+                               d_pstat, d_lines);
+        if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    } else if (cc) {
         if (hipEventRecord(conc->fork, st) != hipSuccess || hipStreamWaitEvent(conc->side, conc->fork, 0) != hipSuccess)
             return hipErrorUnknown;
+#if !BN_SUB_FROB
         hipLaunchKernelGGL(bn::k_bn_check, dim3((npairs + 63) / 64), dim3(64), 0, conc->side, d_in, d_pair_src, npairs,
                            d_pstat);
+#endif
         if (hipEventRecord(conc->join, conc->side) != hipSuccess) return hipErrorUnknown;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        if (layout & GSV_BN_LAYOUT_LINES2)
-            hipLaunchKernelGGL(bn::k_bn_lines2, dim3((2 * npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src,
-                               npairs, d_lines, conc->d_luse);
-        else
-            hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                               d_lines, conc->d_luse);
+        hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs, d_lines,
+                           conc->d_luse, (uint8_t*)nullptr);
         if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     } else if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        if (BN_PREP_SPLIT) {
+        if (!BN_SUB_FROB && BN_PREP_SPLIT) {
+#if !BN_SUB_FROB
             hipLaunchKernelGGL(bn::k_bn_check, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
                                d_pstat);
             hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                               d_lines, (uint8_t*)nullptr);
+                               d_lines, (uint8_t*)nullptr, (uint8_t*)nullptr);
+#endif
         } else {
             hipLaunchKernelGGL(bn::k_bn_prepare, dim3(2 * ((npairs + 63) / 64)), dim3(64), 0, st, d_in, d_pair_src,
                                npairs, d_pstat, d_lines);

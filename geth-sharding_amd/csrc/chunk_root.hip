@@ -372,6 +372,9 @@ GSV_DI void emit_hash(const PNode& nd, const BodyBatch& bb, uint32_t body, const
 
 // ---------------------------------------------------------------- BOTTOM: 16 leaf children
 // leaf j = [0x20, rlp(b)]: b == 0 -> c3 20 81 80; b < 128 -> c2 20 b; else c4 20 82 81 b
+#ifndef GSV_BOT_PREZERO
+#define GSV_BOT_PREZERO 1
+#endif
 constexpr int BOT_BLOCK = 256;
 constexpr int BOT_BUF = 96;
 
@@ -391,6 +394,15 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
     uint32_t payload = 1;  // trailing empty value slot 0x80
 #pragma unroll
     for (int j = 0; j < 16; j++) payload += v[j] == 0 ? 4u : v[j] < 128 ? 3u : 5u;
+#if GSV_BOT_PREZERO
+    // the 88-byte window zeroed by eleven 64-bit stores up front (no per-byte tail loop), the sponge's
+    // 0x01 pad byte stored after the message instead of XOR-ed into the loaded word by lane compares
+    {
+        uint64_t* mz = (uint64_t*)m;
+#pragma unroll
+        for (int k = 0; k < 11; k++) mz[k] = 0;
+    }
+#endif
     uint32_t o = 0;
     if (payload < 56) {
         m[o++] = (uint8_t)(0xc0 + payload);
@@ -413,6 +425,15 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
         }
     }
     m[o++] = 0x80;
+#if GSV_BOT_PREZERO
+    m[o] = 0x01;  // single block: len <= 83 < 136
+    uint64_t a[25];
+    const uint64_t* q = (const uint64_t*)m;
+#pragma unroll
+    for (int k = 0; k < 11; k++) a[k] = q[k];
+#pragma unroll
+    for (int k = 11; k < 25; k++) a[k] = 0;
+#else
     // zero the rest of the 88-byte window, then pad (single block: len <= 83 < 136)
     for (uint32_t k = o; k < 88; k++) m[k] = 0;
     uint64_t a[25];
@@ -426,6 +447,7 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
 #pragma unroll
     for (int k = 0; k < 11; k++)
         if ((uint32_t)k == lane) a[k] ^= 0x01ull << (8 * (o & 7u));
+#endif
     a[16] ^= 0x8000000000000000ULL;
     keccakf(a);
     uint32_t h[8];

@@ -803,18 +803,12 @@ bool bn_miller2(size_t nlanes, int cus) {
     if (const char* e = getenv("GSV_BN_MILLER2")) return atoi(e) != 0;
     return 2 * nlanes <= (size_t)std::max(cus, 1) * 4 * 64;
 }
-// Curve / subgroup checks on a side stream beside the lines and the Miller loop (GSV_BN_LAYOUT_CONC):
-// pays while the lines and Miller waves leave SIMDs idle, i.e. below about one Miller wave per SIMD.
-// GSV_BN_CONC = 0/1 forces the choice (A/B timing).
+// GSV_BN_LAYOUT_CONC, below about one wave per SIMD: the lines kernel at a one-wave register budget (no
+// spills), and in the BN_SUB_FROB = 0 build the curve / subgroup checks on a side stream beside it and
+// the Miller loop.  GSV_BN_CONC = 0/1 forces the choice (A/B timing).
 bool bn_conc(size_t npairs, int cus) {
     if (const char* e = getenv("GSV_BN_CONC")) return atoi(e) != 0;
     return npairs <= (size_t)std::max(cus, 1) * 4 * 64 * 1;
-}
-// Two lanes per pair for the lines (GSV_BN_LAYOUT_LINES2, with the concurrent layout only) while twice
-// the pairs still fit one wave per SIMD.  GSV_BN_LINES2 = 0/1 forces the choice (A/B timing).
-bool bn_lines2(size_t npairs, int cus) {
-    if (const char* e = getenv("GSV_BN_LINES2")) return atoi(e) != 0;
-    return false && 2 * npairs <= (size_t)std::max(cus, 1) * 4 * 64;  // off until measured
 }
 // Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
 // lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
@@ -842,9 +836,8 @@ std::vector<uint64_t> pairing_key(const uint64_t* h_off, size_t n) {
     const char* f = getenv("GSV_BN_FINAL3");
     const char* m = getenv("GSV_BN_MILLER2");
     const char* cc = getenv("GSV_BN_CONC");
-    const char* l2 = getenv("GSV_BN_LINES2");
     std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0, m ? (uint64_t)atoi(m) + 1 : 0,
-                              cc ? (uint64_t)atoi(cc) + 1 : 0, l2 ? (uint64_t)atoi(l2) + 1 : 0};
+                              cc ? (uint64_t)atoi(cc) + 1 : 0};
     key.insert(key.end(), h_off, h_off + n + 1);
     return key;
 }
@@ -910,7 +903,6 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
                (bn_miller2(s.nl, cus) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
                (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0);
-    if ((s.layout & gsv::GSV_BN_LAYOUT_CONC) && bn_lines2(np, cus)) s.layout |= gsv::GSV_BN_LAYOUT_LINES2;
     s.o_src = L.add(np * 8 + 8);
     s.o_pidx = L.add(np * 4 + 4);
     s.o_lfirst = L.add((s.nl + 1) * 4);
