@@ -187,7 +187,39 @@ static BN_NI void fp12_inv_p(fp12* pe, const fp12* pa) {
 #ifndef BN_EXPU_INLINE_MUL
 #define BN_EXPU_INLINE_MUL 1
 #endif
+// BN_EXPU_W4: width-4 signed-window digits of u instead of its NAF: odd powers a, a^3, a^5, a^7 (one
+// cyclotomic squaring and three products up front; a^-d = conj(a^d)), then 13 products in the chain
+// instead of 23 — 16 F_p^12 products per exponentiation instead of 23, the same field element a^u.
+// Digits (bit i < 62; bit 62 is +1): U_W4_NZ nonzero, U_W4_NEG negative, odd-power index
+// (|d| - 1) / 2 in U_W4_I0 (bit 0) / U_W4_I1 (bit 1).
+#ifndef BN_EXPU_W4
+#define BN_EXPU_W4 1
+#endif
+constexpr uint64_t U_W4_NZ = 0x108844442110211ULL, U_W4_NEG = 0x8004400010010ULL;
+constexpr uint64_t U_W4_I0 = 0x8800400110000ULL, U_W4_I1 = 0x100044002110200ULL;
+static_assert((U_W4_NEG | U_W4_I0 | U_W4_I1) == ((U_W4_NEG | U_W4_I0 | U_W4_I1) & U_W4_NZ), "digit masks");
+GSV_DI int u_w4_index(int i) { return (int)((U_W4_I0 >> i) & 1) | ((int)((U_W4_I1 >> i) & 1) << 1); }
 static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
+#if BN_EXPU_W4
+    fp12 tab[4];  // a^(2k+1)
+    tab[0] = *a;
+    {
+        fp12 a2 = fp12_cyclo_sqr_i(*a);
+#pragma unroll 1
+        for (int k = 1; k < 4; k++) fp12_mul_p(&tab[k], &tab[k - 1], &a2);  // out of line: runs 3 times
+    }
+    fp12 sum = *a;  // the leading digit +1
+#pragma unroll 1
+    for (int i = 61; i >= 0; i--) {
+        sum = fp12_cyclo_sqr_i(sum);
+        if ((U_W4_NZ >> i) & 1) {
+            fp12 t = tab[u_w4_index(i)];
+            if ((U_W4_NEG >> i) & 1) t.x = fp6_store(fp6_neg(t.x));
+            sum = fp12_mul_i(sum, t);
+        }
+    }
+    *c = sum;
+#else
     fp12 sum = *a;  // the leading digit: 1^2 * a
 #pragma unroll 1
     for (int i = 61; i >= 0; i--) {
@@ -204,6 +236,7 @@ static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
         }
     }
     *c = sum;
+#endif
 }
 
 // ---- three-lane cooperative exponentiation by u, for batches too small to give every SIMD a wave.
@@ -265,6 +298,31 @@ static BN_NI void fp12_mul3(fp12* pe, const fp12* pa, const fp12* pb, int role, 
     fp12_mul3_i(pe, *pa, *pb, role, base);
 }
 static BN_NI void fp12_exp_u3(fp12* c, const fp12* a, int role, int base) {
+#if BN_EXPU_W4
+    fp12 tab[4];  // a^(2k+1), as fp12_exp_u
+    tab[0] = *a;
+    {
+        fp12 a2;
+        fp12_cyclo_sqr3_i(&a2, *a, role, base);
+#pragma unroll 1
+        for (int k = 1; k < 4; k++) fp12_mul3(&tab[k], &tab[k - 1], &a2, role, base);
+    }
+    fp12 acc = *a;
+#pragma unroll 1
+    for (int i = 61; i >= 0; i--) {
+        fp12 sq;
+        fp12_cyclo_sqr3_i(&sq, acc, role, base);
+        acc = sq;
+        if ((U_W4_NZ >> i) & 1) {
+            fp12 t = tab[u_w4_index(i)];
+            if ((U_W4_NEG >> i) & 1) t.x = fp6_store(fp6_neg(t.x));
+            fp12 m;
+            fp12_mul3_i(&m, acc, t, role, base);
+            acc = m;
+        }
+    }
+    *c = acc;
+#else
     fp12 sum = *a;
 #pragma unroll 1
     for (int i = 61; i >= 0; i--) {
@@ -289,6 +347,7 @@ static BN_NI void fp12_exp_u3(fp12* c, const fp12* a, int role, int base) {
         }
     }
     *c = sum;
+#endif
 }
 
 // ---------------------------------------------------------------- twist points (twist.go)
