@@ -716,7 +716,10 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     # consecutive batches on `depth` streams with their own shape instances (as the chunk-root leg):
     # one batch's latency-bound Miller / final-exponentiation waves share the SIMDs with the next
     # batch's kernels
-    depth = max(1, args.pairing_pipeline)
+    # auto: three batches in flight for the per-rank batch of N > 1 (the layout then turns work-efficient,
+    # 8,192 checks 4.67 -> 3.73 ms per batch), two at 65,536 (3 % slower at three;
+    # profiles/r03/ab_pairing_depth.txt)
+    depth = args.pairing_pipeline if args.pairing_pipeline > 0 else (3 if nloc < 65536 else 2)
     ctx.set_pipeline_depth(depth)
     streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
     pvk = [pver] + [torch.empty_like(pver) for _ in range(depth - 1)]
@@ -877,8 +880,9 @@ def main():
     ap.add_argument("--legs", default=",".join(LEGS), help="comma list of " + ",".join(LEGS))
     ap.add_argument("--pipeline", type=int, default=2,
                     help="streams (shape instances) consecutive chunk-root batches are spread over")
-    ap.add_argument("--pairing-pipeline", type=int, default=2,
-                    help="streams (shape instances) consecutive pairing batches are spread over")
+    ap.add_argument("--pairing-pipeline", type=int, default=0,
+                    help="streams (shape instances) consecutive pairing batches are spread over "
+                         "(0 = auto: 3 below 65,536 checks per rank, else 2)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rank plumbing only (no GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

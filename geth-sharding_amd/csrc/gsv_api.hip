@@ -799,9 +799,11 @@ bool bn_final3(size_t nchecks, int cus) {
 }
 // Two lanes per Miller lane while twice the Miller lanes still fit one wave per SIMD (the Miller
 // kernel's register budget admits one wave per SIMD).  GSV_BN_MILLER2 = 0/1 forces the choice.
-bool bn_miller2(size_t nlanes, int cus) {
+// With three or more batches in flight (pipeline depth) the other batches' kernels fill the SIMDs a
+// small batch leaves idle, so the work-efficient layout wins: no second Miller lane.
+bool bn_miller2(size_t nlanes, int cus, int depth) {
     if (const char* e = getenv("GSV_BN_MILLER2")) return atoi(e) != 0;
-    return 2 * nlanes <= (size_t)std::max(cus, 1) * 4 * 64;
+    return depth < 3 && 2 * nlanes <= (size_t)std::max(cus, 1) * 4 * 64;
 }
 // GSV_BN_LAYOUT_CONC, below about one wave per SIMD: the lines kernel at a one-wave register budget (no
 // spills), and in the BN_SUB_FROB = 0 build the curve / subgroup checks on a side stream beside it and
@@ -814,13 +816,16 @@ bool bn_conc(size_t npairs, int cus) {
 // lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
 // and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
 // batches split a check over more lanes (k = 2, 1).  GSV_BN_PAIRS_PER_LANE forces k (A/B timing).
-uint32_t bn_pairs_per_lane(size_t np, int cus) {
+// At pipeline depth >= 3 a batch only needs a sixth of that (batches overlap): 8,192 checks 4.69 ->
+// 3.66 ms per batch at depth 4 with k = 2 and no second Miller lane, 16,384 6.96 -> 6.04 ms at depth 3
+// with k = 4 (profiles/r03/ab_pairing_layout_pipe.txt).
+uint32_t bn_pairs_per_lane(size_t np, int cus, int depth) {
     if (const char* e = getenv("GSV_BN_PAIRS_PER_LANE")) {
         int k = atoi(e);
         if (k >= 1) return (uint32_t)k;
     }
     const size_t waves = 1;
-    size_t target = (size_t)std::max(cus, 1) * 4 * 64 * waves;
+    size_t target = (size_t)std::max(cus, 1) * 4 * 64 * waves / (depth >= 3 ? 6 : 1);
     for (uint32_t k = 4; k > 1; k >>= 1)
         if ((np + k - 1) / k >= target) return k;
     return 1;
@@ -841,7 +846,8 @@ std::vector<uint64_t> pairing_key(const uint64_t* h_off, size_t n) {
     key.insert(key.end(), h_off, h_off + n + 1);
     return key;
 }
-int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L) {
+// depth: batches the caller keeps in flight on this shape (1 for the synchronous host path)
+int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L, int depth) {
     s.kind = SK_PAIRING;
     int cus = device_cus(c->device);
     std::vector<uint8_t> bad_len(n, 0);
@@ -886,7 +892,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
         }
     }
     check_first[n] = (uint32_t)q;
-    uint32_t kpl = bn_pairs_per_lane(np, cus);
+    uint32_t kpl = bn_pairs_per_lane(np, cus, depth);
     std::vector<uint32_t> check_lane(n + 1), lane_first;
     lane_first.reserve(n + np / kpl + 2);
     for (size_t k = 0; k < n; k++) {
@@ -901,7 +907,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.nl = lane_first.size() - 1;
     s.nchecks = n;
     s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
-               (bn_miller2(s.nl, cus) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
+               (bn_miller2(s.nl, cus, depth) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
                (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0);
     s.o_src = L.add(np * 8 + 8);
     s.o_pidx = L.add(np * 4 + 4);
@@ -1429,8 +1435,9 @@ int gsv_bn256_pairing_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n) {
     std::lock_guard<std::mutex> g(c->smu);
     HIPCHK(hipSetDevice(c->device));
     Shape* s;
+    const int depth = std::max(1, c->pipeline_depth);
     int rc = shape_get(c, SK_PAIRING, pairing_key(h_off, n),
-                       [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, h_off, n, L); }, &s);
+                       [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, h_off, n, L, depth); }, &s);
     if (rc) return rc;
     return pairing_conc_init(*s);
 }
@@ -1464,7 +1471,7 @@ int gsv_bn256_pairing_check_batch(gsv_ctx* c, const uint8_t* in, const uint64_t*
     size_t bytes = off[n] - off[0];
     size_t staged = al(bytes + 8) + al(n);
     Shape s;
-    int rc = shape_temp(c, staged, [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, rel.data(), n, L); }, s);
+    int rc = shape_temp(c, staged, [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, rel.data(), n, L, 1); }, s);
     if (rc) return rc;
     rc = pairing_conc_init(s);
     if (rc) return rc;

@@ -60,8 +60,9 @@ if os.environ.get("SWEEP_CASES"):  # e.g. "4,,1;2,,1" = k,final3,miller2 (empty 
 
 def run_pipelined(ctx, n, depth, steps=12):
     """n checks per batch, consecutive batches over `depth` streams (gsv_ctx_set_pipeline_depth)"""
-    for v in ("GSV_BN_PAIRS_PER_LANE", "GSV_BN_FINAL3", "GSV_BN_MILLER2"):
-        os.environ.pop(v, None)
+    if not os.environ.get("SWEEP_KEEP_LAYOUT"):  # else the GSV_BN_* overrides in the environment apply
+        for v in ("GSV_BN_PAIRS_PER_LANE", "GSV_BN_FINAL3", "GSV_BN_MILLER2"):
+            os.environ.pop(v, None)
     pin = torch.empty((n, 768), dtype=torch.uint8, device="cuda")
     pexp = torch.empty((n,), dtype=torch.uint8, device="cuda")
     ctx.bn256_synth_checks_dev(5000, pin, pexp)
