@@ -156,8 +156,10 @@ def test_synth_checks_match_oracle(ctx, oracle):
 
 
 def test_g2_subgroup_predicate_vs_oracle(ctx, oracle):
-    """The GPU decides G2 membership with the psi-endomorphism criterion; the oracle with the
-    reference's Order*Q double-and-add (twist.go:60-62).  Both must classify identically: random
+    """The GPU decides G2 membership from the Miller-loop line chain's final point
+    (r + psi^3(Q) == O, csrc/bn256.hip g2_frob_check; the number theory in
+    test_g2_frob_relation.py); the oracle with the reference's Order*Q double-and-add
+    (twist.go:60-62).  Both must classify identically: random
     twist points outside G2, pure cofactor-order points [r]X, mixed points X + G, and G2 points."""
     import sys
     sys.path.insert(0, __import__("os").path.dirname(__file__))
