@@ -484,12 +484,25 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     a_rst = torch.full((ws,), -1, dtype=torch.int32, device=dev)
     n_st = torch.empty((max(nloc, 1), NOTARY_TXS), dtype=torch.uint8, device=dev)
     stream.wait_stream(torch.cuda.current_stream())  # the fills above ran on torch's stream
+    # consecutive collation batches kept in flight on `depth` streams (shape instances): one step's
+    # validation overlaps the previous step's tail and all-gather; the library orders the all-gathers
+    # on its communicator.  A rank's block at N = 8 (13 shards) is 1.6k waves, less than one round of
+    # the GPU's 2,048 wave slots, so one step alone leaves it partly idle (tools/notary_sweep.py)
+    depth = max(1, args.notary_pipeline)
+    ctx.set_pipeline_depth(depth)
     ctx.notary_partition_prepare(n_off, N_SHARDS, ws, rank, max_txs=NOTARY_TXS)
+    ctx.set_pipeline_depth(1)
+    n_streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
+    outs = [(a_root, a_ntx, a_bm, a_rst)] + [(torch.zeros_like(a_root), torch.zeros_like(a_ntx), torch.zeros_like(a_bm),
+                                             torch.full_like(a_rst, -1)) for _ in range(depth - 1)]
+    for s_ in n_streams[1:]:
+        s_.wait_stream(torch.cuda.current_stream())
 
-    def notary_step(with_status=False):
-        ctx.notary_validate_partition_dev(nb, n_off, N_SHARDS, a_root, a_ntx, a_bm, None,
-                                          n_st if with_status else None, a_rst, max_txs=NOTARY_TXS, stream=stream,
-                                          prepare=False)
+    def notary_step(with_status=False, i=0):
+        r_, c_, b_, st_ = outs[i % depth]
+        ctx.notary_validate_partition_dev(nb, n_off, N_SHARDS, r_, c_, b_, None,
+                                          n_st if with_status else None, st_, max_txs=NOTARY_TXS,
+                                          stream=n_streams[i % depth], prepare=False)
 
     notary_step(with_status=True)
     stream.synchronize()
@@ -524,14 +537,22 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     g_root, g_ntx, g_bm = SH.unpack_records(gathered, ws, N_SHARDS, NOTARY_TXS)
     assert torch.equal(g_root, a_root) and torch.equal(g_ntx, a_ntx) and torch.equal(g_bm, a_bm), \
         "C-ABI RCCL records differ from the torch.distributed gather"
-    nsteps = max(2, args.steps // 2)
+    nsteps = max(2 * depth, args.steps // 2)
+    for i in range(1, depth):  # warm the other instances
+        notary_step(i=i)
+    for s_ in n_streams:
+        s_.synchronize()
     barrier(ws)
     t4 = time.perf_counter()
-    for _ in range(nsteps):
-        notary_step()
-    stream.synchronize()
+    for i in range(nsteps):
+        notary_step(i=i)
+    for s_ in n_streams:
+        s_.synchronize()
     barrier(ws)
     ndt = max_over_ranks(time.perf_counter() - t4, ws)
+    for r_, c_, b_, st_ in outs:  # every instance's last gathered records equal the checked ones
+        assert torch.equal(r_, a_root) and torch.equal(c_, a_ntx) and torch.equal(b_, a_bm)
+        assert int(st_.min()) == 0 and int(st_.max()) == 0
     ctx.reset_timing()  # kernel breakdown from a separate, instrumented step
     ctx.set_timing(True)
     notary_step()
@@ -543,6 +564,7 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
            "txs_per_s": round(N_SHARDS * NOTARY_TXS * nsteps / ndt, 1),
            "shards": N_SHARDS, "txs_per_shard": NOTARY_TXS, "shards_per_rank": per_rank,
            "ms_per_step": round(ndt / nsteps * 1e3, 3), "tx_kernels_ms_per_step": round(k_not, 3),
+           "pipeline_depth": depth,
            "entry_point": "gsv_notary_validate_partition_dev (C ABI)",
            "collective": "ncclAllGather on the library's RCCL communicator (gsv_comm_init)" if ws > 1
            else "none (1 rank: the block is copied)",
@@ -883,6 +905,8 @@ def main():
     ap.add_argument("--pairing-pipeline", type=int, default=0,
                     help="streams (shape instances) consecutive pairing batches are spread over "
                          "(0 = auto: 3 below 65,536 checks per rank, else 2)")
+    ap.add_argument("--notary-pipeline", type=int, default=2,
+                    help="streams (shape instances) consecutive notary partition steps are spread over")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rank plumbing only (no GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -172,6 +172,10 @@ struct gsv_ctx {
     // RCCL communicator of the shard partition (gsv_comm_init), nullptr = single rank
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // completion of the last all-gather issued on `comm`: the next one, possibly on another stream (a
+    // pipelined partition call), waits for it, so collectives on the communicator never overlap
+    hipEvent_t coll_ev = nullptr;
+    bool coll_rec = false;
     int pipeline_depth = 1;  // instances per prepared shape (gsv_ctx_set_pipeline_depth)
 };
 
@@ -544,6 +548,7 @@ void gsv_ctx_destroy(gsv_ctx* c) {
     for (auto e : c->free_events) hipEventDestroy(e);
     c->shapes.clear();
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->coll_ev) hipEventDestroy(c->coll_ev);
     if (c->arena) hipFree(c->arena);
     if (c->gtab) hipFree(c->gtab);
     hipStreamDestroy(c->stream);
@@ -1215,7 +1220,20 @@ int partition_pack(gsv_ctx* c, const Shape& s, const PartDims& d, const uint8_t*
 // the path's one collective: every rank's block to every rank (one ncclAllGather over xGMI)
 int partition_gather(gsv_ctx* c, const uint8_t* blk, uint8_t* all, const PartDims& d, hipStream_t st) {
     if (c->nranks > 1 && c->comm) {
+        // calls kept in flight on several streams (pipeline depth) overlap their validation, not their
+        // collectives: each all-gather follows the previous one on the communicator (every rank issues
+        // them in the same order).  Inside a graph capture the caller's graph orders them.
+        const bool cap = capturing(st);
+        if (!cap) {
+            if (!c->coll_ev && hipEventCreateWithFlags(&c->coll_ev, hipEventDisableTiming) != hipSuccess)
+                return GSV_E_HIP;
+            if (c->coll_rec && hipStreamWaitEvent(st, c->coll_ev, 0) != hipSuccess) return GSV_E_HIP;
+        }
         if (ncclAllGather(blk, all, d.B, ncclUint8, c->comm, st) != ncclSuccess) return GSV_E_RCCL;
+        if (!cap) {
+            if (hipEventRecord(c->coll_ev, st) != hipSuccess) return GSV_E_HIP;
+            c->coll_rec = true;
+        }
         return GSV_SUCCESS;
     }
     if (c->nranks > 1) return GSV_E_INVALID_ARG;

@@ -334,7 +334,10 @@ int gsv_notary_validate_partition(gsv_ctx *ctx, const uint8_t *bodies, const uin
  * shards have zero records).  A rank-local failure joins the collective as above and returns its code
  * (the other ranks see it in d_rank_status).  gsv_notary_partition_prepare prepares it for exactly
  * (h_off, n_total_shards, nranks, rank, chain id, signer, max_txs); the context's communicator gives
- * nranks / rank. */
+ * nranks / rank.  Prepared at pipeline depth D (gsv_ctx_set_pipeline_depth), D consecutive calls may be
+ * in flight on D streams: their validations overlap, and the library makes each call's all-gather wait
+ * for the previous one on the communicator (an event chain; outside a graph capture), so collectives
+ * never overlap and every rank issues them in call order. */
 int gsv_notary_partition_prepare(gsv_ctx *ctx, const uint64_t *h_off, size_t n_total_shards, int nranks, int rank,
                                  const uint8_t *chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs);
 int gsv_notary_validate_partition_dev(gsv_ctx *ctx, const uint8_t *d_bodies, const uint64_t *h_off,

@@ -49,6 +49,41 @@ def test_partition_one_rank_equals_local_validation(ctx):
     assert (ntx.cpu().numpy() == txs).all() and int(rst[0]) == 0
 
 
+def test_partition_dev_pipelined_on_two_streams(ctx):
+    """Consecutive partition calls kept in flight on two streams (pipeline depth 2, as bench.py's notary
+    leg): each call's records equal the whole-batch validation.  At N > 1 the library orders their
+    all-gathers on the communicator (one-rank communicator here: the gather is a copy)."""
+    import torch
+    nsh, txs = 13, 512
+    dev = torch.device("cuda", ctx.device)
+    bodies_t = torch.empty(nsh * txs * 128, dtype=torch.uint8, device=dev)
+    ctx.notary_synth_dev(78, 0, nsh, txs, bodies_t)
+    torch.cuda.synchronize()
+    flat = bodies_t.cpu().numpy()
+    want = ctx.notary_validate_shards([flat[i * txs * 128:(i + 1) * txs * 128].tobytes() for i in range(nsh)],
+                                      max_txs=txs)
+    ctx.comm_init(gsv.comm_unique_id(), 1, 0)
+    off = np.arange(nsh + 1, dtype=np.uint64) * txs * 128
+    ctx.set_pipeline_depth(2)
+    try:
+        ctx.notary_partition_prepare(off, nsh, 1, 0, max_txs=txs)
+    finally:
+        ctx.set_pipeline_depth(1)
+    ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    outs = [(torch.zeros((nsh, 32), dtype=torch.uint8, device=dev), torch.zeros((nsh,), dtype=torch.int32, device=dev),
+             torch.zeros((nsh, txs // 8), dtype=torch.uint8, device=dev),
+             torch.full((1,), -99, dtype=torch.int32, device=dev)) for _ in range(6)]
+    for s_ in ss:
+        s_.wait_stream(torch.cuda.current_stream())
+    for i, (root, ntx, bm, rst) in enumerate(outs):
+        ctx.notary_validate_partition_dev(bodies_t, off, nsh, root, ntx, bm, rank_status_t=rst, max_txs=txs,
+                                          stream=ss[i % 2], prepare=False)
+    torch.cuda.synchronize()
+    for root, ntx, bm, rst in outs:
+        assert np.array_equal(root.cpu().numpy(), want[0]) and np.array_equal(bm.cpu().numpy(), want[2])
+        assert (ntx.cpu().numpy() == txs).all() and int(rst[0]) == 0
+
+
 def test_partition_local_failure_still_joins_the_collective(ctx):
     """a rank-local failure returns its status after the all-gather, not before it."""
     import torch
