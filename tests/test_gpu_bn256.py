@@ -102,6 +102,46 @@ def test_pairing_miller_lane_split(ctx, oracle, monkeypatch, k):
     assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
 
 
+@pytest.mark.parametrize("k,miller2", [(1, "0"), (1, "1"), (2, "0"), (2, "1")])
+def test_pairing_two_lane_miller_on_off(ctx, oracle, monkeypatch, k, miller2):
+    """The two-lane Miller step (small batches at pipeline depth <= 2) and the one-lane loop (what a
+    shape prepared at depth >= 3 picks) give the oracle's verdicts at every split."""
+    monkeypatch.setenv("GSV_BN_PAIRS_PER_LANE", str(k))
+    monkeypatch.setenv("GSV_BN_MILLER2", miller2)
+    inputs = _random_inputs(oracle, 53 + k)
+    out = ctx.pairing_check_batch(inputs)
+    want = np.array([_v(oracle, x) for x in inputs], np.uint8)
+    assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
+
+
+def test_pairing_dev_prepared_at_depth_three(ctx, oracle):
+    """A device-resident batch prepared at pipeline depth 3 (the depth-aware layout: no two-lane
+    Miller) and run on three streams: every run gives the oracle's verdicts."""
+    import torch
+    inputs = _random_inputs(oracle, 61)
+    want = np.array([_v(oracle, x) for x in inputs], np.uint8)
+    off = np.zeros(len(inputs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in inputs])
+    dev = torch.device("cuda", ctx.device)
+    flat = b"".join(inputs)
+    pin = torch.from_numpy(np.frombuffer(flat, np.uint8).copy()).to(dev)
+    ctx.set_pipeline_depth(3)
+    try:
+        ctx.pairing_prepare(off)
+    finally:
+        ctx.set_pipeline_depth(1)
+    ss = [torch.cuda.Stream(device=dev) for _ in range(3)]
+    outs = [torch.full((len(inputs),), 9, dtype=torch.uint8, device=dev) for _ in range(6)]
+    for s_ in ss:
+        s_.wait_stream(torch.cuda.current_stream())
+    for i, o in enumerate(outs):
+        ctx.pairing_check_batch_dev(pin, off, o, stream=ss[i % 3], prepare=False)
+    torch.cuda.synchronize()
+    for o in outs:
+        got = o.cpu().numpy()
+        assert (got == want).all(), [(i, int(got[i]), int(want[i])) for i in np.nonzero(got != want)[0]]
+
+
 def test_pairing_empty_batch_and_empty_input(ctx):
     assert ctx.pairing_check_batch([]).shape == (0,)
     assert ctx.pairing_check_batch([b""])[0] == 1  # empty input -> true32Byte
