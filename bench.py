@@ -790,7 +790,11 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
             "fp_products_per_check_actual": oc.get("fp_products") if oc else None,
             "kernels_ms_per_step": round(k_tot, 3),
             "per_kernel": {n: {"valu_issue_per_simd_cycle": v.get("valu_issue_per_simd_cycle"),
-                               "traffic": pmc_traffic(v), "vgpr": v.get("vgpr"),
+                               "traffic": pmc_traffic(v),
+                               # rocprofv3's vgpr_count as recorded; on gfx950 it reads half the ISA's
+                               # VGPR + AGPR allocation (k_bn_final 256 for 256 + 256, k_ecrecover 120
+                               # for 234; DESIGN.md §3.4 lists the ISA figures)
+                               "rocprof_vgpr_count": v.get("vgpr"),
                                "scratch_bytes_per_lane": v.get("scratch_bytes_per_lane")} for n, v in kk.items()},
             "algorithmic_per_unit": f"{FP_MULS_PER_CHECK_REF} F_p Montgomery products x {MACS_PER_FP_MUL} partial "
                                     "products per 4-pair check for the reference algorithm (its 254-bit Order*Q "
