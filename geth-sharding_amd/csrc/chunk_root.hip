@@ -375,9 +375,6 @@ GSV_DI void emit_hash(const PNode& nd, const BodyBatch& bb, uint32_t body, const
 #ifndef GSV_BOT_PREZERO
 #define GSV_BOT_PREZERO 1
 #endif
-#ifndef GSV_BOT_BRANCHLESS
-#define GSV_BOT_BRANCHLESS GSV_BOT_PREZERO  // relies on the pad bytes overwriting a short leaf's tail
-#endif
 constexpr int BOT_BLOCK = 256;
 constexpr int BOT_BUF = 96;
 
@@ -413,22 +410,6 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
         m[o++] = 0xf8;
         m[o++] = (uint8_t)payload;
     }
-#if GSV_BOT_BRANCHLESS
-    // every leaf writes five bytes chosen by selects (no divergent branch per leaf) and advances by its
-    // length; the one or two bytes past a short leaf are overwritten by the next leaf, and past the last
-    // one by the 0x80 slot and the 0x01 pad
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint32_t b = v[j];
-        const bool z = b == 0, lo = b < 128;
-        m[o] = (uint8_t)(z ? 0xc3u : lo ? 0xc2u : 0xc4u);
-        m[o + 1] = 0x20;
-        m[o + 2] = (uint8_t)(z ? 0x81u : lo ? b : 0x82u);
-        m[o + 3] = (uint8_t)(z ? 0x80u : 0x81u);
-        m[o + 4] = (uint8_t)b;
-        o += z ? 4u : lo ? 3u : 5u;
-    }
-#else
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         uint8_t b = v[j];
@@ -443,7 +424,6 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
             o += 5;
         }
     }
-#endif
     m[o++] = 0x80;
 #if GSV_BOT_PREZERO
     m[o] = 0x01;  // single block: len <= 83 < 136
