@@ -220,3 +220,30 @@ def test_g2_subgroup_predicate_vs_oracle(ctx, oracle):
     want = [_v(oracle, x) for x in inputs]
     assert list(out) == want
     assert want.count(2) >= 48 and want.count(0) >= 16  # e(G, Q) != 1 for Q in G2 \ {O}
+
+
+def test_g2_membership_at_scale(ctx, oracle):
+    """The line-chain membership test on several hundred points of each class, in one batch (so every
+    lane layout of a mid-sized batch is exercised): twist points outside G2 and their cofactor parts
+    [r]X must be refused (errBadPairingInput, as the reference's Order*Q check refuses them), G2 points
+    plus cofactor points too, and G2 points must be accepted (e(G, Q) != 1: verdict false)."""
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    import bn254_py as B
+    rng = random.Random(29)
+    g1 = oracle.bn256_g1_mul(1)
+    inputs, want = [], []
+    for k in range(120):
+        x = B.twist_point_outside_g2(rng.randrange(1, 1 << 60))
+        h = B.g2_mul(x, B.R)  # the cofactor part of x
+        q = B.g2_decode(oracle.bn256_g2_mul(rng.randrange(1, R)))
+        for p, v in ((x, 2), (h, 2), (B.g2_add(q, h), 2), (q, 0)):
+            if p is None:
+                continue
+            inputs.append(g1 + B.g2_encode(p))
+            want.append(v)
+    out = ctx.pairing_check_batch(inputs)
+    assert list(out) == want, [i for i in range(len(want)) if out[i] != want[i]][:10]
+    # a sample against the oracle's Order*Q, so the expected classes are the reference's
+    for i in range(0, len(inputs), 41):
+        assert _v(oracle, inputs[i]) == want[i]
