@@ -794,8 +794,18 @@ struct LevelLaunch {
     uint32_t gen_blocks;
     int gen_lane;  // 1: one generic node per lane (gen_blocks of 256 lanes), 0: one per wave
 };
+// GSV_LEVEL_WAVES: register budget of the level kernels (waves per SIMD; 0 = the compiler's choice,
+// 100 VGPRs = four waves)
+#ifndef GSV_LEVEL_WAVES
+#define GSV_LEVEL_WAVES 0
+#endif
+#if GSV_LEVEL_WAVES
+#define GSV_LEVEL_ATTR __attribute__((amdgpu_waves_per_eu(GSV_LEVEL_WAVES, GSV_LEVEL_WAVES)))
+#else
+#define GSV_LEVEL_ATTR
+#endif
 template <bool BOT>
-__global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ nodes,
+__global__ __launch_bounds__(256) GSV_LEVEL_ATTR void k_chunk_level(const PNode* __restrict__ nodes,
                                                      const PChild* __restrict__ children, LevelLaunch L,
                                                      BodyBatch bb) {
     __shared__ uint64_t sbuf[(BOT ? 256 * BOT_BUF : 8 * MSG_STRIDE) / 8];
@@ -830,7 +840,10 @@ struct TopLevels {
     uint32_t gen_lane;  // bit h - 1: that height's generic nodes one per lane (throughput form)
 };
 constexpr uint32_t TOP_MAX_BODIES = 256;  // one fused-top workgroup per CU at most
-constexpr int TOP_HFULL_THREADS = 256;  // waves 0-3: HFULL nodes, one per lane
+#ifndef GSV_TOP_HFULL_THREADS
+#define GSV_TOP_HFULL_THREADS 256
+#endif
+constexpr int TOP_HFULL_THREADS = GSV_TOP_HFULL_THREADS;  // waves 0-3: HFULL nodes, one per lane
 #ifndef GSV_TOP_GEN_WAVES
 #define GSV_TOP_GEN_WAVES 2
 #endif
