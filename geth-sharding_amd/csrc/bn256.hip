@@ -78,28 +78,6 @@ GSV_DI bool fp12_is_one(const fp12& e) {
     return (z & (int)fq_eq(e.y.z.y, fq_const(FQ_ONE))) != 0;
 }
 GSV_DI fp12 fp12_conj(const fp12& a) { return fp12{fp6_store(fp6_neg(a.x)), a.y}; }
-// gfp12.go:60-66
-static BN_NI void fp12_frob_p(fp12* pe, const fp12* pa) {
-    const fp12 a = *pa;
-    pe->x = fp6_store(fp6_mul_fp2(fp6_frob(a.x), fp2_const(FQ_XI_P1_6_X, FQ_XI_P1_6_Y)));
-    pe->y = fp6_frob(a.y);
-}
-GSV_DI fp12 fp12_frob(const fp12& a) {
-    fp12 e;
-    fp12_frob_p(&e, &a);
-    return e;
-}
-// gfp12.go:68-74
-static BN_NI void fp12_frob_p2_p(fp12* pe, const fp12* pa) {
-    const fp12 a = *pa;
-    pe->x = fp6_store(fp6_mul_fp(fp6_frob_p2(a.x), fq_c(FQ_XI_PSQ1_6)));
-    pe->y = fp6_frob_p2(a.y);
-}
-GSV_DI fp12 fp12_frob_p2(const fp12& a) {
-    fp12 e;
-    fp12_frob_p2_p(&e, &a);
-    return e;
-}
 // gfp12.go:94-106.  Karatsuba over F_p^6: x = (a.x + a.y)(b.x + b.y) - a.x b.x - a.y b.y equals the
 // reference's a.x b.y + b.x a.y (3 F_p^6 products instead of 4, the same field element).
 GSV_DI fp12 fp12_mul_i(const fp12& a, const fp12& b) {
@@ -107,12 +85,6 @@ GSV_DI fp12 fp12_mul_i(const fp12& a, const fp12& b) {
     auto v1 = fp6_mulx(a.y, b.y);
     fp6 tx = fp6_store(fp6_sub(fp6_sub(fp6_mulx(fp6_add(a.x, a.y), fp6_add(b.x, b.y)), v0), v1));
     return fp12{tx, fp6_store(fp6_add(v1, fp6_mul_tau(v0)))};
-}
-static BN_NI void fp12_mul_p(fp12* pe, const fp12* pa, const fp12* pb) { *pe = fp12_mul_i(*pa, *pb); }
-GSV_DI fp12 fp12_mul(const fp12& a, const fp12& b) {
-    fp12 e;
-    fp12_mul_p(&e, &a, &b);
-    return e;
 }
 // gfp12.go:129-143
 GSV_DI fp12 fp12_sqr_i(const fp12& a) {
@@ -167,84 +139,12 @@ GSV_DI fp12 fp12_cyclo_sqr_i(const fp12& a) {
     e.x.z = r2.hi;
     return e;
 }
-static BN_NI void fp12_cyclo_sqr_p(fp12* pe, const fp12* pa) { *pe = fp12_cyclo_sqr_i(*pa); }
-GSV_DI fp12 fp12_cyclo_sqr(const fp12& a) {
-    fp12 e;
-    fp12_cyclo_sqr_p(&e, &a);
-    return e;
-}
-// gfp12.go:145-160
-static BN_NI void fp12_inv_p(fp12* pe, const fp12* pa) {
-    const fp12 a = *pa;
-    fp6 t1 = fp6_store(fp6_sub(fp6_sqr(a.y), fp6_mul_tau(fp6_sqr(a.x))));
-    fp6 t2 = fp6_inv(t1);
-    pe->x = fp6_store(fp6_mul(fp6_neg(a.x), t2));
-    pe->y = fp6_store(fp6_mul(a.y, t2));
-}
-// gfp12.go:113-127 with power = u; only called on cyclotomic-subgroup elements (the final
-// exponentiation's hard part), where a^-1 = conj(a): the NAF of u needs 23 products instead of the
-// 27 of its binary expansion, and the result is the same field element a^u.
-#ifndef BN_EXPU_INLINE_MUL
-#define BN_EXPU_INLINE_MUL 1
-#endif
-// BN_EXPU_W4: width-4 signed-window digits of u instead of its NAF: odd powers a, a^3, a^5, a^7 (one
-// cyclotomic squaring and three products up front; a^-d = conj(a^d)), then 13 products in the chain
-// instead of 23 — 16 F_p^12 products per exponentiation instead of 23, the same field element a^u.
-// Digits (bit i < 62; bit 62 is +1): U_W4_NZ nonzero, U_W4_NEG negative, odd-power index
-// (|d| - 1) / 2 in U_W4_I0 (bit 0) / U_W4_I1 (bit 1).
-#ifndef BN_EXPU_W4
-#define BN_EXPU_W4 1
-#endif
-constexpr uint64_t U_W4_NZ = 0x108844442110211ULL, U_W4_NEG = 0x8004400010010ULL;
-constexpr uint64_t U_W4_I0 = 0x8800400110000ULL, U_W4_I1 = 0x100044002110200ULL;
-static_assert((U_W4_NEG | U_W4_I0 | U_W4_I1) == ((U_W4_NEG | U_W4_I0 | U_W4_I1) & U_W4_NZ), "digit masks");
-GSV_DI int u_w4_index(int i) { return (int)((U_W4_I0 >> i) & 1) | ((int)((U_W4_I1 >> i) & 1) << 1); }
-static BN_NI void fp12_exp_u(fp12* c, const fp12* a) {
-#if BN_EXPU_W4
-    fp12 tab[4];  // a^(2k+1)
-    tab[0] = *a;
-    {
-        fp12 a2 = fp12_cyclo_sqr_i(*a);
-#pragma unroll 1
-        for (int k = 1; k < 4; k++) fp12_mul_p(&tab[k], &tab[k - 1], &a2);  // out of line: runs 3 times
-    }
-    fp12 sum = *a;  // the leading digit +1
-#pragma unroll 1
-    for (int i = 61; i >= 0; i--) {
-        sum = fp12_cyclo_sqr_i(sum);
-        if ((U_W4_NZ >> i) & 1) {
-            fp12 t = tab[u_w4_index(i)];
-            if ((U_W4_NEG >> i) & 1) t.x = fp6_store(fp6_neg(t.x));
-            sum = fp12_mul_i(sum, t);
-        }
-    }
-    *c = sum;
-#else
-    fp12 sum = *a;  // the leading digit: 1^2 * a
-#pragma unroll 1
-    for (int i = 61; i >= 0; i--) {
-        sum = fp12_cyclo_sqr_i(sum);
-        bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
-        if (pos || neg) {
-            fp12 t = *a;
-            if (neg) t.x = fp6_store(fp6_neg(t.x));
-#if BN_EXPU_INLINE_MUL
-            sum = fp12_mul_i(sum, t);
-#else
-            sum = fp12_mul(sum, t);
-#endif
-        }
-    }
-    *c = sum;
-#endif
-}
-
-// ---- three-lane cooperative exponentiation by u, for batches too small to give every SIMD a wave.
-// The three lanes of a triple (wave lanes base, base+1, base+2) all hold the whole F_p^12 value;
-// each operation is split into three equal parts selected by the lane's role (same instruction
+// ---- three-lane cooperative F_p^12 operations (k_bn_final3), for batches too small to give every
+// SIMD a wave.  The three lanes of a triple (wave lanes base, base+1, base+2) all hold the whole F_p^12
+// value; each operation is split into three equal parts selected by the lane's role (same instruction
 // stream, different operands: no divergence), and the parts are exchanged with ds_bpermute.  The
-// dependent chain per exp_u step becomes a third as long; every part computes the same formula as
-// the one-lane routine, so results are the same field elements.
+// dependent chain per step becomes a third as long; every part computes the same formula as the
+// one-lane routine, so results are the same field elements.
 GSV_DI uint32_t bperm(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_ds_bpermute(lane << 2, (int)v); }
 template <class T>
 GSV_DI void gather3(T out[3], const T& mine, int base) {  // out[r] = lane (base + r)'s `mine`
@@ -281,75 +181,6 @@ GSV_DI void fp12_cyclo_sqr3_i(fp12* pe, const fp12& a, int role, int base) {
     pe->y.x = all[2].lo;
     pe->x.z = all[2].hi;
 }
-static BN_NI void fp12_cyclo_sqr3(fp12* pe, const fp12* pa, int role, int base) {
-    fp12_cyclo_sqr3_i(pe, *pa, role, base);
-}
-// fp12_mul_i's three F_p^6 products, one per role
-GSV_DI void fp12_mul3_i(fp12* pe, const fp12& a, const fp12& b, int role, int base) {
-    fp6 sa = fp6_store(fp6_add(a.x, a.y)), sb = fp6_store(fp6_add(b.x, b.y));
-    fp6 l = role == 0 ? a.x : role == 1 ? a.y : sa;
-    fp6 r = role == 0 ? b.x : role == 1 ? b.y : sb;
-    fp6 prod = fp6_store(fp6_mul(l, r)), v[3];
-    gather3(v, prod, base);
-    pe->x = fp6_store(fp6_sub(fp6_sub(v[2], v[0]), v[1]));
-    pe->y = fp6_store(fp6_add(v[1], fp6_mul_tau(v[0])));
-}
-static BN_NI void fp12_mul3(fp12* pe, const fp12* pa, const fp12* pb, int role, int base) {
-    fp12_mul3_i(pe, *pa, *pb, role, base);
-}
-static BN_NI void fp12_exp_u3(fp12* c, const fp12* a, int role, int base) {
-#if BN_EXPU_W4
-    fp12 tab[4];  // a^(2k+1), as fp12_exp_u
-    tab[0] = *a;
-    {
-        fp12 a2;
-        fp12_cyclo_sqr3_i(&a2, *a, role, base);
-#pragma unroll 1
-        for (int k = 1; k < 4; k++) fp12_mul3(&tab[k], &tab[k - 1], &a2, role, base);
-    }
-    fp12 acc = *a;
-#pragma unroll 1
-    for (int i = 61; i >= 0; i--) {
-        fp12 sq;
-        fp12_cyclo_sqr3_i(&sq, acc, role, base);
-        acc = sq;
-        if ((U_W4_NZ >> i) & 1) {
-            fp12 t = tab[u_w4_index(i)];
-            if ((U_W4_NEG >> i) & 1) t.x = fp6_store(fp6_neg(t.x));
-            fp12 m;
-            fp12_mul3_i(&m, acc, t, role, base);
-            acc = m;
-        }
-    }
-    *c = acc;
-#else
-    fp12 sum = *a;
-#pragma unroll 1
-    for (int i = 61; i >= 0; i--) {
-#if BN_EXPU_INLINE_MUL
-        fp12 s2v;
-        fp12_cyclo_sqr3_i(&s2v, sum, role, base);
-        sum = s2v;
-#else
-        fp12_cyclo_sqr3(&sum, &sum, role, base);
-#endif
-        bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
-        if (pos || neg) {
-            fp12 t = *a;
-            if (neg) t.x = fp6_store(fp6_neg(t.x));
-#if BN_EXPU_INLINE_MUL
-            fp12 m;
-            fp12_mul3_i(&m, sum, t, role, base);
-            sum = m;
-#else
-            fp12_mul3(&sum, &sum, &t, role, base);
-#endif
-        }
-    }
-    *c = sum;
-#endif
-}
-
 // ---------------------------------------------------------------- twist points (twist.go)
 // twist.go:136-162 dbl-2009-l (t is not updated, as in the reference)
 GSV_DI g2j g2_double_i(const g2j& a) {
@@ -564,57 +395,6 @@ GSV_DI void mul_line_i(fp12& ret, const line& l) {
     ret.y = fp6_store(fp6_add(t3, fp6_mul_tau(a2)));
 }
 static BN_NI void mul_line_p(fp12* ret, const line* l) { mul_line_i(*ret, *l); }
-
-// optate.go:212-261
-// base >= 0: the lane is one of the three lanes (base, base+1, base+2) sharing this check (role =
-// its index), which run the three exponentiations by u cooperatively
-static BN_NI void final_exp(fp12* out, const fp12* in, int role, int base) {
-    // every F_p^12 product and cyclotomic squaring goes to the cooperative form on a triple
-    auto MUL = [&](const fp12& a, const fp12& b) {
-        fp12 e;
-        if (base >= 0) fp12_mul3(&e, &a, &b, role, base);
-        else fp12_mul_p(&e, &a, &b);
-        return e;
-    };
-    auto CSQR = [&](const fp12& a) {
-        fp12 e;
-        if (base >= 0) fp12_cyclo_sqr3(&e, &a, role, base);
-        else fp12_cyclo_sqr_p(&e, &a);
-        return e;
-    };
-    // the reference's sequence of products, ordered so that at most six F_p^12 values are live
-    // (they sit in per-lane scratch between the out-of-line calls)
-    fp12 t1 = fp12_conj(*in), t2;
-    fp12_inv_p(&t2, in);
-    t1 = MUL(t1, t2);
-    t1 = MUL(t1, fp12_frob_p2(t1));
-    fp12 y0;  // frob(t1) frob_p2(t1) frob(frob_p2(t1))
-    {
-        fp12 f2 = fp12_frob_p2(t1);
-        y0 = MUL(MUL(fp12_frob(t1), f2), fp12_frob(f2));
-    }
-    fp12 fu, fu2, fu3;
-    if (base >= 0) {
-        fp12_exp_u3(&fu, &t1, role, base);
-        fp12_exp_u3(&fu2, &fu, role, base);
-    } else {
-        fp12_exp_u(&fu, &t1);
-        fp12_exp_u(&fu2, &fu);
-    }
-    fp12 y3 = fp12_conj(fp12_frob(fu));
-    fp12 y4 = fp12_conj(MUL(fu, fp12_frob(fu2)));
-    if (base >= 0) fp12_exp_u3(&fu3, &fu2, role, base);
-    else fp12_exp_u(&fu3, &fu2);
-    fp12 y6 = fp12_conj(MUL(fu3, fp12_frob(fu3)));
-    fp12 y5 = fp12_conj(fu2);
-    fp12 t0 = MUL(MUL(CSQR(y6), y4), y5);
-    t2 = MUL(MUL(y3, y5), t0);
-    t0 = MUL(t0, fp12_frob_p2(fu2));  // y2
-    t2 = CSQR(MUL(CSQR(t2), t0));
-    t0 = MUL(t2, fp12_conj(t1));      // y1
-    t2 = MUL(t2, y0);
-    *out = MUL(CSQR(t0), t2);
-}
 
 // ---------------------------------------------------------------- SoA helpers
 // field element k (of K per item) of item i in a [K*9 words][n] word-major array
@@ -1040,7 +820,298 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
     if (!role) fp12_store(fv, nlanes, c, f);
 }
 
-// role/base as final_exp: the verdict is written by role 0
+// ---------------------------------------------------------------- final exponentiation (optate.go:212-261)
+// The final exponentiation runs as a PROGRAM of F_p^12 operations on two values: X (the accumulator,
+// in registers) and A (the operand, in LDS: one F_p^12 per lane, 27 KB per 64-lane workgroup, so four
+// workgroups still fit a CU).  One loop executes it; its body holds a single copy of each operation,
+// so k_bn_final's code stays small, and nothing is called: no call frames, no callee-saved register
+// spills, no private segment.  A product streams A's halves from LDS, so its working set is X plus
+// one F_p^6 product's (a dense F_p^6 product alone needs ~240 VGPRs of operands and column
+// accumulators; with both F_p^12 operands in registers the kernel spilled 1.3 KB per lane).  Values
+// that outlive X and A go to an explicit per-check workspace in HBM ([slot][108 words][check],
+// coalesced), written and read once each: 7 stores + 8 loads of 432 bytes per check.  The program is
+// the reference's sequence regrouped (the same group element, so the same IsOne verdict):
+//   t1 = conj(in) in^-1,  t1 *= frob^2(t1)                                   (easy part)
+//   fu = t1^u, fu2 = fu^u, fu3 = fu2^u  (NAF of u: 62 cyclotomic squarings, 23 products each)
+//   y0 = frob(t1 frob(t1 frob(t1))) = frob(t1) frob^2(t1) frob^3(t1),  C = y0 y1^2  (y1 = conj t1)
+//   y3 = conj frob(fu), y4 = conj(fu frob(fu2)), y5 = conj fu2, y2 = frob^2(fu2), y6 = conj(fu3 frob(fu3))
+//   B = y4 y5, D = (y3 y5)^2 y2, t0 = y6^2 B,  T = (D t0^3)^2,  result = T^3 C
+// which expands to the reference's t0 = y6^2 y4 y5, t1 = ((y3 y5 t0)^2 t0 y2)^2, (t1 y1)^2 (t1 y0):
+// 15 F_p^12 products outside the exponentiations (as the reference) and two more cyclotomic squarings.
+enum : uint8_t {
+    FE_END = 0,
+    FE_MUL,    // X = X A
+    FE_MULC,   // X = X conj(A)
+    FE_CSQR,   // X = X^2 (cyclotomic)
+    FE_FROB,   // X = frob(X)
+    FE_FROB2,  // X = frob^2(X)
+    FE_CONJ,   // X = conj(X)
+    FE_INV,    // X = X^-1
+    FE_XA,     // A = X
+    FE_AX,     // X = A
+    FE_SWAP,   // X <-> A
+    FE_LDX,    // X = ws[slot]
+    FE_LDA,    // A = ws[slot]
+    FE_STX,    // ws[slot] = X
+    FE_LDFV,   // A = the next Miller-lane value of the check (prologue; not in the program)
+};
+static_assert(BN_FINAL_SLOTS == 4, "the program uses slots 0..3");
+constexpr int FE_MAXOPS = 384;
+struct FeProg {
+    uint8_t op[FE_MAXOPS];
+    int n;
+};
+struct FeBuild {
+    FeProg p{};
+    constexpr void e(int k, int slot = 0) { p.op[p.n++] = (uint8_t)(k | slot << 5); }
+    // X = A^u (gfp12.go:113-127 on the NAF of u, constants.go:17; a^-1 = conj(a) in the cyclotomic
+    // subgroup); A unchanged
+    constexpr void exp_u() {
+        e(FE_AX);  // the leading digit (bit 62)
+        for (int i = 61; i >= 0; i--) {
+            e(FE_CSQR);
+            if ((U_NAF_POS >> i) & 1) e(FE_MUL);
+            if ((U_NAF_NEG >> i) & 1) e(FE_MULC);
+        }
+    }
+    constexpr FeProg build() {
+        // easy part: X = in
+        e(FE_XA), e(FE_INV), e(FE_MULC);             // X = in^-1 conj(in)
+        e(FE_XA), e(FE_FROB2), e(FE_MUL);            // X = t1
+        e(FE_XA);                                    // A = t1
+        exp_u();                                     // X = fu
+        e(FE_STX, 0);                                // s0 = fu
+        e(FE_AX), e(FE_FROB), e(FE_MUL), e(FE_FROB), e(FE_MUL), e(FE_FROB);  // X = y0
+        e(FE_SWAP), e(FE_CSQR), e(FE_SWAP), e(FE_MULC);  // X = y0 conj(t1)^2 = C
+        e(FE_STX, 1);                                // s1 = C
+        e(FE_LDA, 0), e(FE_AX), e(FE_FROB), e(FE_CONJ), e(FE_STX, 2);  // s2 = y3, A = fu
+        exp_u();                                     // X = fu2
+        e(FE_STX, 0);                                // s0 = fu2
+        e(FE_FROB), e(FE_MUL), e(FE_CONJ);           // X = y4
+        e(FE_LDA, 0), e(FE_MULC), e(FE_STX, 3);      // s3 = B = y4 y5, A = fu2
+        e(FE_LDX, 2), e(FE_MULC), e(FE_CSQR), e(FE_STX, 2);  // s2 = (y3 y5)^2
+        e(FE_AX), e(FE_FROB2), e(FE_LDA, 2), e(FE_MUL), e(FE_STX, 2);  // s2 = D
+        e(FE_LDA, 0);                                // A = fu2
+        exp_u();                                     // X = fu3
+        e(FE_XA), e(FE_FROB), e(FE_MUL), e(FE_CONJ);  // X = y6
+        e(FE_CSQR), e(FE_LDA, 3), e(FE_MUL);         // X = t0
+        e(FE_XA), e(FE_CSQR), e(FE_MUL);             // X = t0^3
+        e(FE_LDA, 2), e(FE_MUL), e(FE_CSQR);         // X = T
+        e(FE_XA), e(FE_CSQR), e(FE_MUL);             // X = T^3
+        e(FE_LDA, 1), e(FE_MUL);                     // X = T^3 C
+        e(FE_END);
+        return p;
+    }
+};
+constexpr FeProg fe_program() { return FeBuild{}.build(); }
+__device__ constexpr FeProg FE_PROG = fe_program();
+static_assert(fe_program().n <= FE_MAXOPS, "program length");
+
+GSV_DI fp12 fp12_frob_i(const fp12& a) {  // gfp12.go:60-66
+    return fp12{fp6_store(fp6_mul_fp2(fp6_frob(a.x), fp2_const(FQ_XI_P1_6_X, FQ_XI_P1_6_Y))), fp6_frob(a.y)};
+}
+GSV_DI fp12 fp12_frob_p2_i(const fp12& a) {  // gfp12.go:68-74
+    return fp12{fp6_store(fp6_mul_fp(fp6_frob_p2(a.x), fq_c(FQ_XI_PSQ1_6))), fp6_frob_p2(a.y)};
+}
+GSV_DI fp12 fp12_inv_i(const fp12& a) {  // gfp12.go:145-160
+    fp6 t1 = fp6_store(fp6_sub(fp6_sqr(a.y), fp6_mul_tau(fp6_sqr(a.x))));
+    fp6 t2 = fp6_inv(t1);
+    return fp12{fp6_store(fp6_mul(fp6_neg(a.x), t2)), fp6_store(fp6_mul(a.y, t2))};
+}
+// explicit per-check F_p^12 storage: [slot][108 words][n] (coalesced across the wave)
+GSV_DI fp12 ws_load(const uint32_t* __restrict__ ws, uint32_t n, uint32_t c, int slot) {
+    fp12 e;
+    uint32_t* w = (uint32_t*)&e;
+#pragma unroll
+    for (int k = 0; k < 108; k++) w[k] = ws[((size_t)slot * 108 + k) * n + c];
+    return e;
+}
+GSV_DI void ws_store(uint32_t* __restrict__ ws, uint32_t n, uint32_t c, int slot, const fp12& e) {
+    const uint32_t* w = (const uint32_t*)&e;
+#pragma unroll
+    for (int k = 0; k < 108; k++) ws[((size_t)slot * 108 + k) * n + c] = w[k];
+}
+// A in LDS: word q of the lane's F_p^12 at lds[q * 64] (the lane's column of a [108][64] array: every
+// access is one conflict-free ds_read/write_b32 across the wave)
+GSV_DI fp6 lds_fp6(const uint32_t* lds, int half) {
+    fp6 e;
+    uint32_t* w = (uint32_t*)&e;
+#pragma unroll
+    for (int q = 0; q < 54; q++) w[q] = lds[(half * 54 + q) * 64];
+    return e;
+}
+GSV_DI fp12 lds_fp12(const uint32_t* lds) { return fp12{lds_fp6(lds, 0), lds_fp6(lds, 1)}; }
+GSV_DI void lds_put(uint32_t* lds, const fp12& e) {
+    const uint32_t* w = (const uint32_t*)&e;
+#pragma unroll
+    for (int q = 0; q < 108; q++) lds[q * 64] = w[q];
+}
+// A.x of the operand, conjugated (negated) for FE_MULC
+GSV_DI fp6 lds_ax(const uint32_t* lds, bool conj) {
+    fp6 ax = lds_fp6(lds, 0);
+    if (conj) ax = fp6_store(fp6_neg(ax));
+    return ax;
+}
+// an F_p element below 2^256 (limbs normalised, value < 3p) packed into eight words and back: the
+// 29-bit limbs are the value's base-2^29 digits, so the round trip is exact
+GSV_DI void fq_pack_lds(uint32_t* lds, const fqm<1, 3>& a) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            int lo = 29 * i - 32 * j;  // bit of word j where limb i starts
+            if (lo >= 32 || lo + 29 <= 0) continue;
+            w |= lo >= 0 ? a.v[i] << lo : a.v[i] >> -lo;
+        }
+        lds[j * 64] = w;
+    }
+}
+GSV_DI fqm<1, 3> fq_unpack_lds(const uint32_t* lds) {
+    uint32_t w[9];
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = lds[j * 64];
+    w[8] = 0;
+    fqm<1, 3> r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        int k = 29 * i / 32, sh = 29 * i % 32;
+        uint32_t v = sh ? (w[k] >> sh) | (w[k + 1] << (32 - sh)) : w[k];
+        r.v[i] = v & FQ_M29;
+    }
+    return r;
+}
+// X = X A (fp12_mul_i; A = lds, conjugated when conj).  The three F_p^6 products run one after the
+// other (scheduling barriers keep the scheduler from interleaving them), A's halves are read from LDS
+// where each product needs them, v0 waits in LDS (reduced below 3p and packed into 48 words, next to
+// A's 108: 156 words per lane, 39 KB per workgroup) and v1 and X.x + X.y take X's registers — so each
+// product runs with only one other F_p^6 value live beside it, and nothing spills.
+constexpr int FE_LDS_V0 = 108;  // word offset of the packed v0 in the lane's LDS column
+GSV_DI void fp12_mul_lds(fp12& X, uint32_t* lds, bool conj) {
+    {
+        auto v0 = fp6_mul(X.x, lds_ax(lds, conj));
+        fq_pack_lds(lds + (FE_LDS_V0 + 0) * 64, fq_reduce(v0.x.x));
+        fq_pack_lds(lds + (FE_LDS_V0 + 8) * 64, fq_reduce(v0.x.y));
+        fq_pack_lds(lds + (FE_LDS_V0 + 16) * 64, fq_reduce(v0.y.x));
+        fq_pack_lds(lds + (FE_LDS_V0 + 24) * 64, fq_reduce(v0.y.y));
+        fq_pack_lds(lds + (FE_LDS_V0 + 32) * 64, fq_reduce(v0.z.x));
+        fq_pack_lds(lds + (FE_LDS_V0 + 40) * 64, fq_reduce(v0.z.y));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    X.x = fp6_store(fp6_add(X.x, X.y));
+    X.y = fp6_store(fp6_mul(X.y, lds_fp6(lds, 1)));  // v1
+    __builtin_amdgcn_sched_barrier(0);
+    fp6 v2 = fp6_store(fp6_mul(X.x, fp6_add(lds_ax(lds, conj), lds_fp6(lds, 1))));
+    __builtin_amdgcn_sched_barrier(0);
+    using e3 = fp2m<1, 3>;
+    fp6t<e3> v0{e3{fq_unpack_lds(lds + (FE_LDS_V0 + 0) * 64), fq_unpack_lds(lds + (FE_LDS_V0 + 8) * 64)},
+                e3{fq_unpack_lds(lds + (FE_LDS_V0 + 16) * 64), fq_unpack_lds(lds + (FE_LDS_V0 + 24) * 64)},
+                e3{fq_unpack_lds(lds + (FE_LDS_V0 + 32) * 64), fq_unpack_lds(lds + (FE_LDS_V0 + 40) * 64)}};
+    X.x = fp6_store(fp6_sub(fp6_sub(v2, v0), X.y));
+    X.y = fp6_store(fp6_add(X.y, fp6_mul_tau(v0)));
+}
+// the three-lane form of fp12_mul_i: role 0 X.x A.x, role 1 X.y A.y, role 2 (X.x + X.y)(A.x + A.y)
+GSV_DI void fp12_mul3_lds(fp12& X, const uint32_t* lds, bool conj, int role, int base) {
+    fp6 l = role == 0 ? X.x : role == 1 ? X.y : fp6_store(fp6_add(X.x, X.y));
+    fp6 ax = lds_ax(lds, conj), ay = lds_fp6(lds, 1);
+    fp6 r = role == 0 ? ax : role == 1 ? ay : fp6_store(fp6_add(ax, ay));
+    fp6 prod = fp6_store(fp6_mul(l, r)), v[3];
+    gather3(v, prod, base);
+    X.x = fp6_store(fp6_sub(fp6_sub(v[2], v[0]), v[1]));
+    X.y = fp6_store(fp6_add(v[1], fp6_mul_tau(v[0])));
+}
+
+// FinalArgs: maxl = the most Miller lanes any check of the batch has (the prologue's length, uniform
+// across the wave); ws = the final exponentiation's workspace, BN_FINAL_SLOTS F_p^12 values per check
+struct FinalArgs {
+    const uint32_t* check_lane;
+    uint32_t nchecks;
+    const uint8_t* cbad;
+    const uint8_t* lstat;
+    const uint32_t* fv;
+    uint32_t nlanes;
+    uint8_t* verdict;
+    uint32_t* ws;
+    uint32_t maxl;
+};
+// Per-lane quantities the machine needs at every operation (the check index, the lane's LDS column,
+// the triple's role and base) are recomputed from the lane id when used instead of being carried
+// across the loop: at the product's register peak every loop-carried VGPR beyond X is one the
+// allocator would otherwise spill to scratch and reload around each product.  The lane id comes from
+// a volatile v_mbcnt pair so the compiler cannot hoist it out of the loop.
+GSV_DI uint32_t lane_id_v() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+// three lanes per check (21 triples per wave, lane 63 idle); a triple's lanes take the same path
+constexpr uint32_t FINAL3_PER_WAVE = 21;
+template <bool COOP>
+struct FeLane {
+    uint32_t lane;
+    GSV_DI FeLane() : lane(lane_id_v()) {}
+    GSV_DI uint32_t t() const { return COOP ? lane / 3 : lane; }
+    GSV_DI uint32_t check() const { return blockIdx.x * (COOP ? FINAL3_PER_WAVE : 64u) + t(); }
+    GSV_DI int role() const { return COOP ? (int)(lane - 3 * t()) : 0; }
+    GSV_DI int base() const { return COOP ? (int)(3 * t()) : -1; }
+};
+// the check's Miller-lane value l0 + 1 + k (one for a lane the check does not have or whose pairs were
+// all at infinity)
+GSV_DI fp12 fv_extra(const FinalArgs& fa, uint32_t c, uint32_t k) {
+    uint32_t l = fa.check_lane[c] + 1 + k;
+    return (l < fa.check_lane[c + 1] && fa.lstat[l] == CS_OK) ? fp12_load(fa.fv, fa.nlanes, l) : fp12_one();
+}
+// The machine.  COOP: the lane is one of three (base, base+1, base+2) sharing the check (role = its
+// index); each F_p^12 product and cyclotomic squaring is split three ways and exchanged (the other
+// operations are cheap and run on all three lanes).  The prologue multiplies in the check's
+// Miller-lane values after the first (nextra of them, uniform across the wave; the product is exact).
+template <bool COOP>
+GSV_DI fp12 final_exp_run(fp12 X, const FinalArgs& fa, uint32_t* lds_base, uint32_t nextra) {
+    const uint32_t npro = 2 * nextra;
+#pragma unroll 1
+    for (uint32_t pc = 0;; pc++) {
+        uint32_t op = pc < npro ? ((pc & 1) ? (uint32_t)FE_MUL : (uint32_t)FE_LDFV) : (uint32_t)FE_PROG.op[pc - npro];
+        uint32_t k = op & 31, slot = op >> 5;
+        if (k == FE_END) break;
+        const FeLane<COOP> ln;
+        uint32_t* lds = lds_base + ln.lane;
+        switch (k) {
+        case FE_MUL:
+        case FE_MULC:
+            if constexpr (COOP) fp12_mul3_lds(X, lds, k == FE_MULC, ln.role(), ln.base());
+            else fp12_mul_lds(X, lds, k == FE_MULC);
+            break;
+        case FE_CSQR:
+            if constexpr (COOP) {
+                fp12 m;
+                fp12_cyclo_sqr3_i(&m, X, ln.role(), ln.base());
+                X = m;
+            } else {
+                X = fp12_cyclo_sqr_i(X);
+            }
+            break;
+        case FE_FROB: X = fp12_frob_i(X); break;
+        case FE_FROB2: X = fp12_frob_p2_i(X); break;
+        case FE_CONJ: X = fp12_conj(X); break;
+        case FE_INV: X = fp12_inv_i(X); break;
+        case FE_XA: lds_put(lds, X); break;
+        case FE_AX: X = lds_fp12(lds); break;
+        case FE_SWAP: {
+            fp12 t = lds_fp12(lds);
+            lds_put(lds, X);
+            X = t;
+            break;
+        }
+        case FE_LDX: X = ws_load(fa.ws, fa.nchecks, ln.check(), (int)slot); break;
+        case FE_LDA: lds_put(lds, ws_load(fa.ws, fa.nchecks, ln.check(), (int)slot)); break;
+        case FE_STX: ws_store(fa.ws, fa.nchecks, ln.check(), (int)slot, X); break;
+        case FE_LDFV: lds_put(lds, fv_extra(fa, ln.check(), pc >> 1)); break;
+        default: break;
+        }
+    }
+    return X;
+}
+
 // cbad[c] != 0: the check's input length is not a multiple of 192 (errBadPairingInput,
 // core/vm/contracts.go:336-338); it has no pairs
 // PairBad (concurrent layout): the check kernel's per-pair verdicts, read here because the Miller
@@ -1050,54 +1121,36 @@ struct PairBad {
     const uint32_t* pidx;
     const uint8_t* pstat;  // nullptr: the Miller loop already saw pstat (lstat CS_BAD)
 };
-GSV_DI void final_check(uint32_t c, const uint32_t* __restrict__ check_lane, const uint8_t* __restrict__ cbad,
-                        const uint8_t* __restrict__ lstat, const uint32_t* __restrict__ fv, uint32_t nlanes,
-                        uint8_t* __restrict__ verdict, int role, int base, const PairBad& pb) {
-    uint32_t l0 = check_lane[c], l1 = check_lane[c + 1];
-    bool bad = cbad[c] != 0;
-    for (uint32_t l = l0; l < l1; l++) bad = bad || lstat[l] == CS_BAD;
+// the verdict is written by the lane of role 0
+template <bool COOP>
+GSV_DI void final_check(const FinalArgs& fa, const PairBad& pb, uint32_t* lds_base) {
+    const FeLane<COOP> ln;
+    if (COOP && ln.t() >= FINAL3_PER_WAVE) return;
+    uint32_t c = ln.check();
+    if (c >= fa.nchecks) return;
+    uint32_t l0 = fa.check_lane[c], l1 = fa.check_lane[c + 1];
+    bool bad = fa.cbad[c] != 0;
+    for (uint32_t l = l0; l < l1; l++) bad = bad || fa.lstat[l] == CS_BAD;
     if (pb.pstat)
         for (uint32_t q = pb.lane_first[l0]; q < pb.lane_first[l1]; q++) bad = bad || pb.pstat[pb.pidx[q]] == PS_BAD;
     if (bad) {
-        if (role == 0) verdict[c] = GSV_PAIRING_BAD_INPUT;
+        if (ln.role() == 0) fa.verdict[c] = GSV_PAIRING_BAD_INPUT;
         return;
     }
-    // product of the check's lane values; finalExponentiation(1) == 1 when no pair is finite
-    fp12 acc;
-    bool any = false;
-    for (uint32_t l = l0; l < l1; l++) {
-        if (lstat[l] != CS_OK) continue;
-        if (!any) {
-            acc = fp12_load(fv, nlanes, l);
-            any = true;
-        } else {
-            acc = fp12_mul(acc, fp12_load(fv, nlanes, l));
-        }
-    }
-    if (!any) acc = fp12_one();
-    fp12 r;
-    final_exp(&r, &acc, role, base);
-    if (role == 0) verdict[c] = fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
+    // the product of the check's finite lane values (finalExponentiation(1) == 1 when there are none):
+    // X = the first lane's value, the prologue multiplies in the rest
+    fp12 X = (l0 < l1 && fa.lstat[l0] == CS_OK) ? fp12_load(fa.fv, fa.nlanes, l0) : fp12_one();
+    fp12 r = final_exp_run<COOP>(X, fa, lds_base, fa.maxl > 1 ? fa.maxl - 1 : 0);
+    if (ln.role() == 0) fa.verdict[c] = fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
 }
 
-__global__ __launch_bounds__(64) void k_bn_final(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
-                                                 const uint8_t* __restrict__ cbad, const uint8_t* __restrict__ lstat,
-                                                 const uint32_t* __restrict__ fv, uint32_t nlanes,
-                                                 uint8_t* __restrict__ verdict, PairBad pb) {
-    uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchecks) return;
-    final_check(c, check_lane, cbad, lstat, fv, nlanes, verdict, 0, -1, pb);
+__global__ __launch_bounds__(64) void k_bn_final(FinalArgs fa, PairBad pb) {
+    __shared__ uint32_t lds[(FE_LDS_V0 + 48) * 64];  // per lane: the machine's operand A, a product's v0
+    final_check<false>(fa, pb, lds);
 }
-// three lanes per check (21 triples per wave, lane 63 idle); a triple's lanes take the same path
-constexpr uint32_t FINAL3_PER_WAVE = 21;
-__global__ __launch_bounds__(64) void k_bn_final3(const uint32_t* __restrict__ check_lane, uint32_t nchecks,
-                                                  const uint8_t* __restrict__ cbad, const uint8_t* __restrict__ lstat,
-                                                  const uint32_t* __restrict__ fv, uint32_t nlanes,
-                                                  uint8_t* __restrict__ verdict, PairBad pb) {
-    int t = threadIdx.x / 3, role = threadIdx.x - 3 * t;
-    uint32_t c = blockIdx.x * FINAL3_PER_WAVE + t;
-    if (t >= (int)FINAL3_PER_WAVE || c >= nchecks) return;
-    final_check(c, check_lane, cbad, lstat, fv, nlanes, verdict, role, 3 * t, pb);
+__global__ __launch_bounds__(64) void k_bn_final3(FinalArgs fa, PairBad pb) {
+    __shared__ uint32_t lds[108 * 64];
+    final_check<true>(fa, pb, lds);
 }
 
 
@@ -1166,7 +1219,17 @@ GSV_DI void g1_mul_gen(fq& ox, fq& oy, const uint32_t k[8]) {
     ox = fq_store(fq_mul(sum.x, zi2));
     oy = fq_store(fq_mul(sum.y, fq_mul(zi2, zi)));
 }
-GSV_DI void g2_mul_gen(g2a& o, const uint32_t k[8]) {
+// a fixed point on the twist outside G2 (x = 12345 + 86416 i, tests/bn254_py.py
+// twist_point_outside_g2(12345)), in the precompile encoding (imaginary part first)
+__device__ constexpr uint8_t SYNTH_T[128] = {
+    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x01, 0x51, 0x90,
+    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x30, 0x39,
+    0x2f, 0x7a, 0xba, 0x3d, 0x52, 0xda, 0x8d, 0x8d, 0x95, 0x21, 0x32, 0xa9, 0x9c, 0xd9, 0xdc, 0x90,
+    0x4e, 0x51, 0x0a, 0x61, 0x17, 0x56, 0x54, 0xbe, 0x75, 0xa9, 0x5d, 0x0d, 0x2a, 0x12, 0xfc, 0x1d,
+    0x13, 0x76, 0x85, 0x1a, 0x42, 0x91, 0x39, 0x13, 0xf7, 0xaf, 0xd2, 0x6c, 0x8b, 0x1c, 0x1a, 0x33,
+    0x6d, 0xb5, 0xce, 0xd0, 0x33, 0x1c, 0x5c, 0x20, 0xbc, 0x3e, 0x7c, 0xdc, 0x57, 0xde, 0xdc, 0x27};
+// k Q (Q the G2 generator), plus T (outside G2) when add_t: the sum is then on the twist and outside G2
+GSV_DI void g2_mul_gen(g2a& o, const uint32_t k[8], bool add_t) {
     g2j base{fp2_const(FQ_TWIST_GEN_XX, FQ_TWIST_GEN_XY), fp2_const(FQ_TWIST_GEN_YX, FQ_TWIST_GEN_YY), fp2_one(),
              fp2_one()};
     g2j sum{fp2_zero(), fp2_one(), fp2_zero(), fp2_zero()};
@@ -1176,6 +1239,15 @@ GSV_DI void g2_mul_gen(g2a& o, const uint32_t k[8]) {
         g2_double_p(&t, &sum);
         if ((k[b >> 5] >> (b & 31)) & 1u) g2_add_p(&sum, &t, &base);
         else sum = t;
+    }
+    if (add_t) {
+        g2j tj{fp2_zero(), fp2_zero(), fp2_one(), fp2_one()}, r;
+        fp_unmarshal(tj.x.x, SYNTH_T);
+        fp_unmarshal(tj.x.y, SYNTH_T + 32);
+        fp_unmarshal(tj.y.x, SYNTH_T + 64);
+        fp_unmarshal(tj.y.y, SYNTH_T + 96);
+        g2_add_p(&r, &sum, &tj);
+        sum = r;
     }
     fp2 zi = fp2_inv(sum.z);
     fp2 zi2 = s2(fp2_sqr(zi));
@@ -1199,7 +1271,15 @@ GSV_DI void synth_scalar(uint32_t k[8], uint64_t seed, uint64_t i, uint32_t tag)
     k[7] &= 0x1FFFFFFFu;  // < 2^253 < r
     if ((k[0] | k[1] | k[2] | k[3] | k[4] | k[5] | k[6] | k[7]) == 0) k[0] = 1;
 }
-// one (G1, G2) pair of the check: lane (check, j) for j = 0..3
+// one (G1, G2) pair of the check: lane (check, j) for j = 0..3.  Classes by c mod 1024 (besides the
+// false checks, c mod 8 == 7, whose fourth pair uses -(d+1)P):
+//   100: pairs 0 and 1 have G1 = infinity (skipped by PairingCheck, bn256.go:318) -> true
+//   200: pairs 0 and 1 have G2 = infinity -> true
+//   300: pair 1 is (infinity, bQ + T) with T outside G2: G2.Unmarshal rejects it before the infinity
+//        pair is skipped (core/vm/contracts.go:341-352, twist.go:60-62) -> bad input
+//   400: pair 1 is (infinity, bQ with y.re's low bit flipped): off the twist -> bad input
+//   500: pair 3's G2 point is cQ + T (outside G2) -> bad input
+//   1023: pair 2's G1 x coordinate == p -> bad input
 __global__ __launch_bounds__(64) void k_bn_synth(uint64_t seed, uint32_t nchecks, uint8_t* __restrict__ out,
                                                  uint8_t* __restrict__ expect) {
     uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1212,7 +1292,12 @@ __global__ __launch_bounds__(64) void k_bn_synth(uint64_t seed, uint32_t nchecks
     uint32_t ty = (j == 0) ? tags[1] : (j == 1) ? tags[0] : (j == 2) ? tags[3] : tags[2];
     synth_scalar(s1, seed, c, tx);
     synth_scalar(s2w, seed, c, ty);
-    bool is_false = (c % 8u) == 7u, is_bad = (c % 1024u) == 1023u;
+    const uint32_t cls = c % 1024u;
+    bool is_false = (c % 8u) == 7u, is_bad = cls == 1023u || cls == 300u || cls == 400u || cls == 500u;
+    bool inf_g1 = (cls == 100u && j <= 1u) || ((cls == 300u || cls == 400u) && j == 1u);
+    bool inf_g2 = cls == 200u && j <= 1u;
+    bool add_t = (cls == 300u && j == 1u) || (cls == 500u && j == 3u);
+    bool off_twist = cls == 400u && j == 1u;
     if (j == 3 && is_false) {  // d + 1 (no overflow: d < 2^253)
         uint64_t cy = 1;
 #pragma unroll
@@ -1226,7 +1311,7 @@ __global__ __launch_bounds__(64) void k_bn_synth(uint64_t seed, uint32_t nchecks
     g1_mul_gen(px, py, s1);
     if (j & 1u) py = fq_store(fq_neg(py));  // -xP
     g2a q;
-    g2_mul_gen(q, s2w);
+    g2_mul_gen(q, s2w, add_t);
     uint8_t* o = out + (size_t)c * 768 + j * 192;
     fp_marshal(o, px);
     fp_marshal(o + 32, py);
@@ -1234,7 +1319,12 @@ __global__ __launch_bounds__(64) void k_bn_synth(uint64_t seed, uint32_t nchecks
     fp_marshal(o + 96, q.x.y);
     fp_marshal(o + 128, q.y.x);
     fp_marshal(o + 160, q.y.y);
-    if (j == 2 && is_bad) {  // coordinate == p: bn256 "coordinate equals modulus"
+    if (inf_g1)
+        for (int i = 0; i < 64; i++) o[i] = 0;
+    if (inf_g2)
+        for (int i = 64; i < 192; i++) o[i] = 0;
+    if (off_twist) o[191] ^= 1u;  // stays < p unless y.re == p - 1 (then coordinate == p: also bad)
+    if (j == 2 && cls == 1023u) {  // coordinate == p: bn256 "coordinate equals modulus"
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             uint32_t w = BN_P_W[7 - i];
@@ -1250,6 +1340,8 @@ __global__ __launch_bounds__(64) void k_bn_synth(uint64_t seed, uint32_t nchecks
 
 }  // namespace bn
 
+bool bn256_layout_forks() { return !BN_SUB_FROB; }
+
 hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st) {
     if (nchecks == 0) return hipSuccess;
     uint32_t lanes = nchecks * 4u;
@@ -1261,7 +1353,7 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
                                 uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
-                                uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
+                                uint32_t* d_fws, uint32_t maxl, uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
                                 void (*timer_end)(void*, int), void* tctx, const BnConcurrent* conc) {
     // GSV_BN_LAYOUT_CONC: the curve / subgroup checks run on a side stream beside the lines, the Miller
     // loop (on the lines role's PS_OK / PS_SKIP) and join before the final exponentiation, which reads
@@ -1330,12 +1422,12 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         if (e != hipSuccess) return e;
         if (cc && hipStreamWaitEvent(st, conc->join, 0) != hipSuccess) return hipErrorUnknown;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
+        bn::FinalArgs fa{d_check_lane, nchecks, d_cbad, d_lstat, d_fv, nlanes, d_verdict, d_fws, maxl};
         if (layout & GSV_BN_LAYOUT_FINAL3)
             hipLaunchKernelGGL(bn::k_bn_final3, dim3((nchecks + bn::FINAL3_PER_WAVE - 1) / bn::FINAL3_PER_WAVE),
-                               dim3(64), 0, st, d_check_lane, nchecks, d_cbad, d_lstat, d_fv, nlanes, d_verdict, pb);
+                               dim3(64), 0, st, fa, pb);
         else
-            hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, d_check_lane, nchecks,
-                               d_cbad, d_lstat, d_fv, nlanes, d_verdict, pb);
+            hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, fa, pb);
         if (timer_end) timer_end(tctx, GSV_K_BN_FINAL);
     } else if (cc && hipStreamWaitEvent(st, conc->join, 0) != hipSuccess) {
         return hipErrorUnknown;

@@ -90,10 +90,13 @@ struct Shape {
     size_t np = 0, nl = 0, nchecks = 0;
     int layout = 0;  // GSV_BN_LAYOUT_* flags
     size_t o_src = 0, o_pidx = 0, o_lfirst = 0, o_clane = 0, o_cbad = 0, o_pstat = 0, o_lines = 0,
-           o_lstat = 0, o_fv = 0, o_luse = 0;
+           o_lstat = 0, o_fv = 0, o_luse = 0, o_fws = 0;
+    uint32_t maxl = 1;  // the most Miller lanes of any check
+    bool deep = false;  // laid out for three or more batches in flight (pairing_shape's depth >= 3)
     // GSV_BN_LAYOUT_CONC: per instance, the side stream and fork/join events (created at prepare)
     std::vector<hipStream_t> side;
     std::vector<hipEvent_t> efork, ejoin;
+    bool side_borrowed = false;  // host-path shape: the context's side stream and events, not its own
     // SK_NOTARY
     uint32_t max_txs = 0, sfx_len = 0;
     int signer_kind = 0;
@@ -117,12 +120,14 @@ struct Shape {
     Shape(const Shape&) = delete;
     Shape& operator=(const Shape&) = delete;
     ~Shape() {
-        for (hipEvent_t e : efork)
-            if (e) hipEventDestroy(e);
-        for (hipEvent_t e : ejoin)
-            if (e) hipEventDestroy(e);
-        for (hipStream_t q : side)
-            if (q) hipStreamDestroy(q);
+        if (!side_borrowed) {
+            for (hipEvent_t e : efork)
+                if (e) hipEventDestroy(e);
+            for (hipEvent_t e : ejoin)
+                if (e) hipEventDestroy(e);
+            for (hipStream_t q : side)
+                if (q) hipStreamDestroy(q);
+        }
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : bulk_ev)
@@ -176,6 +181,10 @@ struct gsv_ctx {
     // pipelined partition call), waits for it, so collectives on the communicator never overlap
     hipEvent_t coll_ev = nullptr;
     bool coll_rec = false;
+    std::mutex cmu;  // the collective: coll_ev / coll_rec and the ncclAllGather issue order
+    // the host paths' side stream and fork/join events (lent to their per-call shapes)
+    hipStream_t hside = nullptr;
+    hipEvent_t hfork = nullptr, hjoin = nullptr;
     int pipeline_depth = 1;  // instances per prepared shape (gsv_ctx_set_pipeline_depth)
 };
 
@@ -549,6 +558,9 @@ void gsv_ctx_destroy(gsv_ctx* c) {
     c->shapes.clear();
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->coll_ev) hipEventDestroy(c->coll_ev);
+    if (c->hfork) hipEventDestroy(c->hfork);
+    if (c->hjoin) hipEventDestroy(c->hjoin);
+    if (c->hside) hipStreamDestroy(c->hside);
     if (c->arena) hipFree(c->arena);
     if (c->gtab) hipFree(c->gtab);
     hipStreamDestroy(c->stream);
@@ -900,17 +912,20 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     uint32_t kpl = bn_pairs_per_lane(np, cus, depth);
     std::vector<uint32_t> check_lane(n + 1), lane_first;
     lane_first.reserve(n + np / kpl + 2);
+    s.maxl = 1;
     for (size_t k = 0; k < n; k++) {
         check_lane[k] = (uint32_t)lane_first.size();
         uint32_t b = check_first[k], e = check_first[k + 1];
         lane_first.push_back(b);  // a check without pairs still gets one (empty) lane
         for (uint32_t p = b + kpl; p < e; p += kpl) lane_first.push_back(p);
+        s.maxl = std::max<uint32_t>(s.maxl, (uint32_t)(lane_first.size() - check_lane[k]));
     }
     check_lane[n] = (uint32_t)lane_first.size();
     lane_first.push_back((uint32_t)q);
     s.np = np;
     s.nl = lane_first.size() - 1;
     s.nchecks = n;
+    s.deep = depth >= 3;
     s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
                (bn_miller2(s.nl, cus, depth) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
                (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0);
@@ -924,6 +939,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.o_lstat = L.add(s.nl + 1);
     s.o_luse = L.add(np + 1);
     s.o_fv = L.add(s.nl * 108 * 4 + 4);
+    s.o_fws = L.add(n * 108 * 4 * gsv::BN_FINAL_SLOTS + 4);  // the final exponentiation's F_p^12 values
     s.stage(s.o_src, pair_src.data(), np);
     s.stage(s.o_pidx, pidx.data(), np);
     s.stage(s.o_lfirst, lane_first.data(), lane_first.size());
@@ -945,9 +961,24 @@ int shape_side_init(Shape& s) {
     }
     return GSV_SUCCESS;
 }
-int pairing_conc_init(Shape& s) {
-    if (!(s.layout & gsv::GSV_BN_LAYOUT_CONC)) return GSV_SUCCESS;
-    return shape_side_init(s);
+// a host-path (per-call) shape borrows the context's side stream and events instead of creating its own
+int shape_side_borrow(gsv_ctx* c, Shape& s) {
+    if (!s.side.empty()) return GSV_SUCCESS;
+    if (!c->hside) {
+        HIPCHK(hipStreamCreateWithFlags(&c->hside, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&c->hfork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->hjoin, hipEventDisableTiming));
+    }
+    s.side.assign(1, c->hside);
+    s.efork.assign(1, c->hfork);
+    s.ejoin.assign(1, c->hjoin);
+    s.side_borrowed = true;
+    return GSV_SUCCESS;
+}
+// the concurrent layout forks onto a side stream only in the BN_SUB_FROB = 0 build (check waves)
+int pairing_conc_init(gsv_ctx* c, Shape& s, bool host_path) {
+    if (!(s.layout & gsv::GSV_BN_LAYOUT_CONC) || !gsv::bn256_layout_forks()) return GSV_SUCCESS;
+    return host_path ? shape_side_borrow(c, s) : shape_side_init(s);
 }
 int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verdict, hipStream_t st) {
     gsv::BnConcurrent conc{};
@@ -961,7 +992,7 @@ int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verd
         d_in, s.at<uint64_t>(s.o_src), (uint32_t)s.np, s.at<uint32_t>(s.o_lfirst), s.at<uint32_t>(s.o_pidx),
         (uint32_t)s.nl, s.at<uint32_t>(s.o_clane), s.at<uint8_t>(s.o_cbad), (uint32_t)s.nchecks,
         s.at<uint8_t>(s.o_pstat), s.at<uint32_t>(s.o_lines), s.at<uint8_t>(s.o_lstat),
-        s.at<uint32_t>(s.o_fv), d_verdict, layout, st, hook_begin, hook_end, c, pc));
+        s.at<uint32_t>(s.o_fv), s.at<uint32_t>(s.o_fws), s.maxl, d_verdict, layout, st, hook_begin, hook_end, c, pc));
 }
 
 // ---- notary: key = chain id, signer, max_txs, body offsets
@@ -1219,7 +1250,8 @@ int partition_pack(gsv_ctx* c, const Shape& s, const PartDims& d, const uint8_t*
 }
 // the path's one collective: every rank's block to every rank (one ncclAllGather over xGMI)
 int partition_gather(gsv_ctx* c, const uint8_t* blk, uint8_t* all, const PartDims& d, hipStream_t st) {
-    if (c->nranks > 1 && c->comm) {
+    if (c->comm) {  // any communicator, one rank included: the same chain on every rank count
+        std::lock_guard<std::mutex> g(c->cmu);  // callers hold mu (error path) or smu (success path)
         // calls kept in flight on several streams (pipeline depth) overlap their validation, not their
         // collectives: each all-gather follows the previous one on the communicator (every rank issues
         // them in the same order).  Inside a graph capture the caller's graph orders them.
@@ -1244,10 +1276,13 @@ int partition_gather(gsv_ctx* c, const uint8_t* blk, uint8_t* all, const PartDim
 template <typename B>
 int shape_get(gsv_ctx* c, uint64_t kind, std::vector<uint64_t>&& key, B&& build, Shape** out) {
     Shape* s = shape_find(c, kind, key);
-    if (s && s->ninst < c->pipeline_depth) {
-        // prepared before the depth was raised: build a deeper one, and RETIRE the old one instead of
-        // freeing it (it is never found again but keeps its memory until LRU eviction, which drains
-        // its queued work first), so a graph captured from it stays valid until then
+    // a pairing shape's layout depends on the depth class it was prepared at (three or more batches in
+    // flight pick the work-efficient layout, pairing_shape): a prepare at the other class rebuilds it
+    const bool reclass = s && kind == SK_PAIRING && s->deep != (c->pipeline_depth >= 3);
+    if (s && (s->ninst < c->pipeline_depth || reclass)) {
+        // prepared before the depth was raised (or at the other depth class): build a new one, and
+        // RETIRE the old one instead of freeing it (it is never found again but keeps its memory until
+        // LRU eviction, which drains its queued work first), so a graph captured from it stays valid
         s->kind |= 1ull << 63;
         s = nullptr;
     }
@@ -1457,7 +1492,7 @@ int gsv_bn256_pairing_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n) {
     int rc = shape_get(c, SK_PAIRING, pairing_key(h_off, n),
                        [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, h_off, n, L, depth); }, &s);
     if (rc) return rc;
-    return pairing_conc_init(*s);
+    return pairing_conc_init(c, *s, false);
 }
 
 int gsv_bn256_pairing_check_batch_dev(gsv_ctx* c, const uint8_t* d_in, const uint64_t* h_off, size_t n,
@@ -1491,7 +1526,7 @@ int gsv_bn256_pairing_check_batch(gsv_ctx* c, const uint8_t* in, const uint64_t*
     Shape s;
     int rc = shape_temp(c, staged, [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, rel.data(), n, L, 1); }, s);
     if (rc) return rc;
-    rc = pairing_conc_init(s);
+    rc = pairing_conc_init(c, s, true);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_in = cv.take<uint8_t>(bytes + 8);
@@ -1526,7 +1561,9 @@ static int notary_args(const uint8_t* chain_id, size_t chain_id_len, int signer_
     if ((chain_id_len && !chain_id) || chain_id_len > 64 || signer_kind < GSV_SIGNER_EIP155 ||
         signer_kind > GSV_SIGNER_FRONTIER)
         return GSV_E_INVALID_ARG;
-    if (n_shards > 65535 || max_txs == 0) return GSV_E_INVALID_ARG;
+    // every blob takes at least one 32-byte chunk, so a body of at most 2^20 bytes holds at most
+    // GSV_MAX_TXS_PER_SHARD = 32,768 of them (also keeps the partition's record offsets in 32 bits)
+    if (n_shards > 65535 || max_txs == 0 || max_txs > GSV_MAX_TXS_PER_SHARD) return GSV_E_INVALID_ARG;
     return GSV_SUCCESS;
 }
 
@@ -1589,7 +1626,7 @@ int gsv_notary_validate_shards(gsv_ctx* c, const uint8_t* bodies, const uint64_t
                     },
                     s);
     if (rc) return rc;
-    rc = shape_side_init(s);
+    rc = shape_side_borrow(c, s);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_b = cv.take<uint8_t>(pos + 16);
@@ -1811,7 +1848,7 @@ int gsv_notary_validate_partition(gsv_ctx* c, const uint8_t* bodies, const uint6
                                                  max_txs, L);
                          },
                          s);
-        if (!lrc && n) lrc = shape_side_init(s);
+        if (!lrc && n) lrc = shape_side_borrow(c, s);
     }
     if (lrc && arena_reserve(c, out_bytes)) return lrc;  // cannot even join the collective
     Carve cv(c->arena);

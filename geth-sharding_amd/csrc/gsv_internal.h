@@ -67,15 +67,20 @@ struct BnConcurrent {
 // runs the multi-Miller loop over pidx[lane_first[l] .. lane_first[l+1]), check c owns lanes
 // [check_lane[c], check_lane[c+1]); cbad[c] != 0 marks a ragged input length (no pairs, verdict
 // BAD_INPUT).  Workspaces (F_p elements are 9 words, bn254_fe9.cuh): pstat[npairs],
-// lines[91 * 54][npairs], lstat[nlanes], fv[108][nlanes] words.  final3: the final exponentiation runs on three cooperating lanes per check
-// (small batches)
+// lines[91 * 54][npairs], lstat[nlanes], fv[108][nlanes] words, fws[BN_FINAL_SLOTS * 108][nchecks]
+// words (the final exponentiation's values that outlive its registers); maxl = the most lanes any
+// check has.  final3: the final exponentiation runs on three cooperating lanes per check (small batches)
+constexpr int BN_FINAL_SLOTS = 4;
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
                                 uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
-                                uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
+                                uint32_t* d_fws, uint32_t maxl, uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
                                 void (*timer_end)(void*, int), void* tctx, const BnConcurrent* conc);
 
+// false in the default build: the concurrent layout only picks the one-wave lines kernel and nothing
+// forks onto a side stream (true in the BN_SUB_FROB = 0 build, whose check waves run beside the lines)
+bool bn256_layout_forks();
 hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st);
 
 // notary.hip

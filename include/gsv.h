@@ -230,7 +230,10 @@ int gsv_bn256_synth_checks_dev(gsv_ctx *ctx, uint64_t seed, size_t nchecks, uint
  * (LSB first) set when tx t's sender recovered (GSV_ST_OK).  Optional per tx, laid out
  * [n_shards][max_txs]: senders_out (20 B, zero when not OK) and status_out (GSV_ST_*).
  * A shard with more than max_txs blobs: only the first max_txs are validated; the host entry point
- * returns GSV_E_TOO_LARGE for it (the _dev one reports it through ntx > max_txs). */
+ * returns GSV_E_TOO_LARGE for it (the _dev one reports it through ntx > max_txs).
+ * 1 <= max_txs <= GSV_MAX_TXS_PER_SHARD (every blob takes at least one 32-byte chunk of a body of at
+ * most 2^20 bytes), else GSV_E_INVALID_ARG; at most 65,535 shards per call. */
+#define GSV_MAX_TXS_PER_SHARD 32768
 int gsv_notary_validate_shards(gsv_ctx *ctx, const uint8_t *bodies, const uint64_t *off, size_t n_shards,
                                const uint8_t *chain_id, size_t chain_id_len, int signer_kind, uint32_t max_txs,
                                uint8_t *root32_out, uint32_t *ntx_out, uint8_t *valid_bitmap_out,

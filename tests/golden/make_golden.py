@@ -261,8 +261,7 @@ def config_fixtures():
                   SHA-256 of the 2^20 addresses (+ of the inputs), first rows;
       configs[2]  100 xoshiro256** bodies of 1 MiB (seeds 0..99): their 100 chunk roots (restated
                   DeriveSha, pinned by tests/test_oracle.py);
-      configs[4]  the bench's 4-pair checks (seed 5000), first 1,024: inputs rebuilt from the oracle's
-                  G1/G2 scalar multiples, verdicts from the oracle's cloudflare restatement."""
+      configs[4]  the bench's 65,536 4-pair checks (seed 5000), see configs4_pairing."""
     import ctypes
     import hashlib
     import threading
@@ -329,30 +328,106 @@ def config_fixtures():
     roots = [None] * 100
     par(lambda i: roots.__setitem__(i, O.derive_sha_bytes(bodies[i])), list(range(100)))
     out["configs2_chunk_roots"] = {"seeds": list(range(100)), "n": 1 << 20, "roots": [h(r) for r in roots]}
-    # configs[4]
-    RR = 21888242871839275222246405745257275088548364400416034343698204186575808495617
-    PP = 21888242871839275222246405745257275088696311157297823662689037894645226208583
-    seed4, m = 5000, 1024
+    out["configs4_pairing"] = configs4_pairing(par)
+    dump("configs.json", out)
 
-    def scal(i, tag):
-        hh = O.keccak256(seed4.to_bytes(8, "little") + i.to_bytes(8, "little") + bytes([tag, 0, 0]))
+
+_T_CACHE = []
+
+
+def _synth_t():
+    """k_bn_synth's SYNTH_T: tests/bn254_py.py twist_point_outside_g2(12345)"""
+    if not _T_CACHE:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import bn254_py as B
+        _T_CACHE.append(B.twist_point_outside_g2(12345))
+    return _T_CACHE[0]
+
+
+def configs4_inputs(c: int, seed4: int = 5000) -> bytes:
+    """Check c of the bench's configs[4] batch, rebuilt on the CPU exactly as k_bn_synth builds it
+    (csrc/bn256.hip): e(aP, bQ) e(-bP, aQ) e(cP, dQ) e(-d'P, cQ) with a, b, c, d = Keccak-256(le64(seed)
+    || le64(c) || tag || 01) truncated to 253 bits, d' = d + 1 when c % 8 == 7 (false), and the classes by
+    c % 1024: 100 pairs 0-1 G1 = infinity (true), 200 pairs 0-1 G2 = infinity (true), 300 pair 1 =
+    (infinity, bQ + T) with T outside G2 (bad input), 400 pair 1 = (infinity, bQ with y.re's low bit
+    flipped: off the twist; bad input), 500 pair 3's G2 point = cQ + T (bad input), 1023 pair 2's G1
+    x = p (bad input)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bn254_py as B
+    RR, PP = B.R, B.P
+
+    def scal(tag):
+        hh = O.keccak256(seed4.to_bytes(8, "little") + c.to_bytes(8, "little") + bytes([tag, 0, 0]))
         return int.from_bytes(hh, "little") & ((1 << 253) - 1) or 1
-    checks = [None] * m
-    verdicts = [None] * m
+    a, b, cc, d = (scal(t) for t in (0x61, 0x62, 0x63, 0x64))
+    d1 = d + 1 if c % 8 == 7 else d
+    cls = c % 1024
+    T = _synth_t()
+    pairs = [[O.bn256_g1_mul(a), O.bn256_g2_mul(b)], [O.bn256_g1_mul(-b % RR), O.bn256_g2_mul(a)],
+             [O.bn256_g1_mul(cc), O.bn256_g2_mul(d)], [O.bn256_g1_mul(-d1 % RR), O.bn256_g2_mul(cc)]]
+    if cls == 100:
+        pairs[0][0] = pairs[1][0] = bytes(64)
+    if cls == 200:
+        pairs[0][1] = pairs[1][1] = bytes(128)
+    if cls in (300, 400):
+        pairs[1][0] = bytes(64)
+    if cls == 300:
+        pairs[1][1] = B.g2_encode(B.g2_add(B.g2_decode(pairs[1][1]), T))
+    if cls == 400:
+        q = bytearray(pairs[1][1])
+        q[127] ^= 1
+        pairs[1][1] = bytes(q)
+    if cls == 500:
+        pairs[3][1] = B.g2_encode(B.g2_add(B.g2_decode(pairs[3][1]), T))
+    inp = b"".join(g1 + g2 for g1, g2 in pairs)
+    if cls == 1023:
+        inp = inp[:384] + PP.to_bytes(32, "big") + inp[416:]
+    return inp
+
+
+def configs4_pairing(par, n: int = 65536, seed4: int = 5000):
+    """configs[4] at full size: the SHA-256 of all 65,536 inputs (rebuilt on the CPU, configs4_inputs)
+    and of their 65,536 verdicts from the oracle's cloudflare restatement (which decides G2 membership
+    with Order*Q, twist.go:60-62), the first 1,024 verdicts in clear, and the verdict count per class."""
+    import hashlib
+    checks = [None] * n
+    verdicts = bytearray(n)
 
     def build(c):
-        a, b, cc, d = (scal(c, t) for t in (0x61, 0x62, 0x63, 0x64))
-        d1 = d + 1 if c % 8 == 7 else d
-        inp = (O.bn256_g1_mul(a) + O.bn256_g2_mul(b) + O.bn256_g1_mul(-b % RR) + O.bn256_g2_mul(a) +
-               O.bn256_g1_mul(cc) + O.bn256_g2_mul(d) + O.bn256_g1_mul(-d1 % RR) + O.bn256_g2_mul(cc))
-        if c % 1024 == 1023:
-            inp = inp[:384] + PP.to_bytes(32, "big") + inp[416:]
+        inp = configs4_inputs(c, seed4)
         checks[c] = inp
         v = O.pairing_check(inp)
         verdicts[c] = 2 if v < 0 else v
-    par(build, list(range(m)))
-    out["configs4_pairing"] = {"seed": seed4, "n": m, "inputs_sha256": hashlib.sha256(b"".join(checks)).hexdigest(),
-                               "verdicts": "".join(str(v) for v in verdicts)}
+    par(build, list(range(n)))
+    counts = {str(v): verdicts.count(v) for v in (0, 1, 2)}
+    return {"seed": seed4, "n": n, "inputs_sha256": hashlib.sha256(b"".join(checks)).hexdigest(),
+            "verdicts_sha256": hashlib.sha256(bytes(verdicts)).hexdigest(), "verdict_counts": counts,
+            "first": 1024, "verdicts": "".join(str(v) for v in verdicts[:1024])}
+
+
+def configs4_fixtures():
+    """Regenerates only configs[4] in configs.json (the rest is left as committed)."""
+    import threading
+
+    def par(fn, items, threads=8):
+        it = iter(items)
+        lk = threading.Lock()
+
+        def w():
+            while True:
+                with lk:
+                    x = next(it, None)
+                if x is None:
+                    return
+                fn(x)
+        ths = [threading.Thread(target=w) for _ in range(threads)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    path = os.path.join(OUT, "configs.json")
+    out = json.load(open(path))
+    out["configs4_pairing"] = configs4_pairing(par)
     dump("configs.json", out)
 
 
@@ -576,6 +651,12 @@ def bn256_fixtures():
     off = B.twist_point_outside_g2(12345)
     add(g1 + B.g2_encode(off), "G2 on the twist but not in the order-r subgroup (bad)")
     add(g1 + g2 + g1 + B.g2_encode(B.twist_point_outside_g2(777)), "second pair outside G2 (bad)")
+    # an all-zero G1 does not excuse its G2 point: Run unmarshals both before PairingCheck skips the
+    # infinity pair (core/vm/contracts.go:341-352, twist.go:47-63, bn256.go:318)
+    add(inf1 + B.g2_encode(off), "G1 infinity with G2 on the twist outside G2 (bad)")
+    add(inf1 + bytes(qs), "G1 infinity with G2 off the twist (bad)")
+    add(g1 + g2 + inf1 + B.g2_encode(B.twist_point_outside_g2(4242)), "second pair: G1 infinity, G2 outside G2 (bad)")
+    add(inf1 + bytes(q), "G1 infinity with a G2 coordinate == p (bad)")
     add(g1 + g2 + b"\x00", "length 193 (bad)")
     add((g1 + g2)[:191], "length 191 (bad)")
     add(b"", "empty input (true)")
@@ -651,7 +732,7 @@ def collation_fixtures():
 FIXTURES = {"keccak": keccak_fixtures, "ecrecover": ecrecover_fixtures, "tx": tx_fixtures,
             "trie": trie_fixtures, "chunk_root": chunk_root_fixtures, "bn256": bn256_fixtures,
             "collation": collation_fixtures, "configs": config_fixtures, "configs3": configs3_fixtures,
-            "chunk_root_large": chunk_root_large_fixtures}
+            "chunk_root_large": chunk_root_large_fixtures, "configs4": configs4_fixtures}
 
 if __name__ == "__main__":
     if not O.ref_available():

@@ -43,6 +43,17 @@ def test_bench_three_ranks_uneven_partition():
     assert line["config"]["rank0_shards"] == [0, 33]
 
 
+def test_bench_eight_ranks_configs3_geometry():
+    """the driver's N = 8 run, rehearsed on the CPU: 100 shards over 8 ranks (12 or 13 per rank),
+    records gathered in blocks padded to 13 over gloo and unpacked in shard order"""
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--dry-run", "--steps", "2"], env=_env(),
+                       capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = _json_line(p.stdout)
+    assert line["n_gpus"] == 8 and line["config"]["shards_per_rank"] == 13
+    assert line["config"]["rank0_shards"] == [0, 12]
+
+
 def test_world_size_must_match_gpus():
     e = _env()
     e.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")

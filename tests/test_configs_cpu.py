@@ -61,7 +61,18 @@ def test_configs2_first_root(oracle):
 
 
 def test_configs4_sample_verdicts(oracle):
+    """The committed configs[4] verdicts follow the generator's classes (make_golden.configs4_inputs),
+    and a sample of checks rebuilt on the CPU gets the committed verdict from the oracle."""
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_golden import configs4_inputs
     g = golden("configs.json")["configs4_pairing"]
     v = g["verdicts"]
-    assert len(v) == 1024 and v.count("2") == 1 and v[1023] == "2"
-    assert all(v[i] == ("0" if i % 8 == 7 else "1") for i in range(1023))
+    assert g["n"] == 65536 and len(v) == g["first"] == 1024
+    bad = {300, 400, 500, 1023}
+    assert all(v[i] == ("2" if i in bad else "0" if i % 8 == 7 else "1") for i in range(1024))
+    per = g["n"] // 1024
+    assert g["verdict_counts"] == {"0": per * 127, "1": per * 893, "2": per * 4}  # 1023 is bad, not false
+    for c in (0, 7, 100, 200, 300, 400, 500, 1023, 1024 + 300, 65535):
+        r = oracle.pairing_check(configs4_inputs(c, g["seed"]))
+        want = 2 if c % 1024 in bad else 0 if c % 8 == 7 else 1
+        assert (2 if r < 0 else r) == want, c

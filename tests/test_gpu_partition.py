@@ -181,11 +181,13 @@ def _rank_worker(rank, world, port, nsh, txs, q):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_ranks_on_one_gpu_validate_blocks_and_gather(world):
+@pytest.mark.parametrize("world,nsh,txs", [(2, 7, 256), (3, 7, 256), (4, 100, 64), (8, 100, 64)])
+def test_ranks_on_one_gpu_validate_blocks_and_gather(world, nsh, txs):
     """world rank processes on the one GPU: each validates its shard block
     (sharding/node/backend.go:245-284 partition) and the gathered records equal a whole-batch
-    validation: the GPU validation composed with the partition's all-gather, across processes."""
+    validation: the GPU validation composed with the partition's all-gather, across processes.
+    (4, 100) and (8, 100) are configs[3]'s geometry at N = 4 and 8: 25 shards per rank, and 12 or 13
+    shards per rank in blocks padded to 13 records, unpacked at the offsets of ranks 1..7."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -194,11 +196,10 @@ def test_ranks_on_one_gpu_validate_blocks_and_gather(world):
     s.close()
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
-    nsh, txs = 7, 256
     ps = [ctxm.Process(target=_rank_worker, args=(r, world, port, nsh, txs, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=100) for _ in range(world))
+    res = dict(q.get(timeout=240) for _ in range(world))
     for p in ps:
         p.join(timeout=30)
     assert res == {r: True for r in range(world)}, res
