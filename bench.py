@@ -52,6 +52,11 @@ MACS_PER_RECOVERY_REF = 1358 * 64 + 1729 * 36 + 301 * 64
 FP_MULS_PER_CHECK_REF = 106852            # tests/test_oracle.py pins the figure
 MACS_PER_FP_MUL = 128                      # Montgomery product: 64 + 64 partial products
 PERMS_PER_MIB = 83016                      # Keccak-f permutations per 1 MiB chunk root (data-independent)
+# The Keccak-f[1600] instruction floor on 32-bit VALU (fixed, not the measured count, so instruction
+# bloat shows in `frac`): per round, theta's column parities 2 v_xor3 per half-column (20), rot(C, 1)
+# 2 v_alignbit per column (10), A ^= C[x-1] ^ rot(C[x+1]) one v_xor3 per word (50); rho 2 v_alignbit
+# per rotated lane (48); chi one v_bitop3 per word (50); iota 2 v_xor: 180 per round, 24 rounds.
+KECCAK_VALU_FLOOR_PER_PERM = 24 * 180
 # Peaks (profiles/r02/microbench_{int,lat}.txt, tools/microbench_*.hip on MI355X):
 #   VALU issue: CDNA4 SIMDs are 32 wide, a wave64 instruction issues over 2 cycles -> at most 0.5
 #   wave-instructions per SIMD per cycle (MI355X_MICROARCH.md, cdna_hip_programming.md §CDNA4).
@@ -89,6 +94,20 @@ def pmc_traffic(k):
     if "fetch_bytes_x2" in k and "write_bytes" in k:
         return int(k["fetch_bytes_x2"] + k["write_bytes"])
     return None
+
+
+def clock_fracs(units_per_launch, k, peak_units_per_s):
+    """The roofline fraction from the PROFILED kernel time (k["avg_ms"], a rocprofv3 trace of the same
+    leg), at the nominal 2.4 GHz peak and at the clock the profiled run held (k["profiled_clock_ghz"]:
+    GRBM_GUI_ACTIVE / duration), beside the bench's own HIP-event figure."""
+    if not k.get("avg_ms") or not peak_units_per_s:
+        return {}
+    a = units_per_launch / (k["avg_ms"] * 1e-3)
+    out = {"frac_profiled_time": round(a / peak_units_per_s, 4)}
+    if k.get("profiled_clock_ghz"):
+        out["profiled_clock_ghz"] = k["profiled_clock_ghz"]
+        out["frac_at_profiled_clock"] = round(a / (peak_units_per_s * k["profiled_clock_ghz"] * 1e9 / CLOCK), 4)
+    return out
 
 
 def opcount(unit):
@@ -362,6 +381,7 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"), "valu_issue_peak": VALU_ISSUE_PEAK,
             "int_lane_ops": int_lane_ops(k, k.get("avg_ms")),
             "kernel": "k_ecrecover", "kernel_avg_ms": round(k_avg_ms, 4),
+            **clock_fracs(MACS_PER_RECOVERY_REF * N_SIGS, k, PEAK_MAC),
             "algorithmic_per_unit": "256-bit products as 8x8 32x32-bit partial products (mul 64, sqr 36): "
                                     f"{MACS_PER_RECOVERY_REF} per recovery for the reference algorithm "
                                     "(libsecp256k1 Strauss-wNAF), mac_equiv_per_recovery_actual = the "
@@ -419,16 +439,18 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
     bot_perms = N_SHARDS * BODY // 16
     k = pmc("void gsv::k_chunk_level<true>", "pmc_chunk_root.json")
     ipp = k["sq_insts_valu"] / bot_perms * 64 if k.get("sq_insts_valu") else None  # VALU instr per perm per lane
-    ceiling = SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / ipp if ipp else None
+    ceiling = SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / KECCAK_VALU_FLOOR_PER_PERM
     traffic = pmc_traffic(k)
     bot_ach = bot_perms / (bot_ms * 1e-3)
     roof = {"bound": "valu", "unit": "Gperm/s", "kernel": "k_chunk_level<BOTTOM>", "kernel_avg_ms": round(bot_ms, 4),
             "achieved": round(bot_ach / 1e9, 3), "peak": round(ceiling / 1e9, 3) if ceiling else None,
             "frac": round(bot_ach / ceiling, 4) if ceiling else None,
             "peak_basis": f"instruction floor: {VALU_ISSUE_PEAK} wave64 VALU instructions per SIMD-cycle x 1024 "
-                          "SIMDs x 2.4 GHz x 64 lanes / VALU instructions per permutation (PMC SQ_INSTS_VALU of a "
-                          f"chunk-root-only pass, profiles/{ROUND}/pmc_chunk_root.json)",
+                          f"SIMDs x 2.4 GHz x 64 lanes / {KECCAK_VALU_FLOOR_PER_PERM} VALU instructions per "
+                          "permutation (the fixed Keccak-f floor, bench.py KECCAK_VALU_FLOOR_PER_PERM)",
             "valu_instr_per_permutation": round(ipp, 1) if ipp else None,
+            "valu_instr_over_floor": round(ipp / KECCAK_VALU_FLOOR_PER_PERM, 3) if ipp else None,
+            **clock_fracs(bot_perms, k, ceiling),
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
             # the body bytes read + every bottom node's raw 32-byte hash written into its parent's slot
             "traffic": traffic, "algorithmic_bytes_per_launch": N_SHARDS * BODY + bot_perms * 32,
@@ -625,15 +647,17 @@ def leg_keccak(ctx, stream, dev, ws, rank, args):
     perms = int(np.sum(lens // 136 + 1))
     k = pmc("gsv::k_keccak256", "pmc_keccak.json")
     ipp = k["sq_insts_valu"] / perms * 64 if k.get("sq_insts_valu") else None
-    ceiling = SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / ipp if ipp else None
+    ceiling = SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / KECCAK_VALU_FLOOR_PER_PERM
     ach = perms / (kavg * 1e-3)
     traffic = pmc_traffic(k)
     roof = {"bound": "valu", "unit": "Gperm/s", "kernel": "k_keccak256", "kernel_avg_ms": round(kavg, 4),
             "achieved": round(ach / 1e9, 3), "peak": round(ceiling / 1e9, 3) if ceiling else None,
             "frac": round(ach / ceiling, 4) if ceiling else None,
-            "peak_basis": "instruction floor (as chunk_root.roofline; PMC of a keccak-only pass, "
-                          f"profiles/{ROUND}/pmc_keccak.json)",
+            "peak_basis": "instruction floor (as chunk_root.roofline: the fixed Keccak-f floor of "
+                          f"{KECCAK_VALU_FLOOR_PER_PERM} VALU instructions per permutation)",
             "valu_instr_per_permutation": round(ipp, 1) if ipp else None,
+            "valu_instr_over_floor": round(ipp / KECCAK_VALU_FLOOR_PER_PERM, 3) if ipp else None,
+            **clock_fracs(perms, k, ceiling),
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
             "traffic": traffic, "algorithmic_bytes_per_launch": int(voff[-1]) + (nblk * ntx + 1) * 8 + nblk * ntx * 32,
             "hbm_GBps": round(traffic / (k["avg_ms"] * 1e-3) / 1e9, 1) if traffic and k.get("avg_ms") else None,
@@ -774,17 +798,20 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     k_mill, _ = ctx.kernel_time(_lib.K_PAIRING)
     k_fin, _ = ctx.kernel_time(_lib.K_BN_FINAL)
     k_tot = (k_prep + k_mill + k_fin) / psteps
-    ref_ach = FP_MULS_PER_CHECK_REF * MACS_PER_FP_MUL * nloc / (k_tot * 1e-3)
     oc = opcount("pairing_check")
     act = oc["mac_equiv"] * nloc / (k_tot * 1e-3) if oc else None
     kk = {n: pmc(f"gsv::bn::{n}", "pmc_pairing.json") for n in ("k_bn_prepare", "k_bn_miller", "k_bn_final")}
-    # headline = the v_mad_u64_u32 our kernels execute (frac_actual); the reference-equivalent figure
-    # counts the reference's 254-bit Order*Q subgroup work, which this path does not do, so it is kept
-    # apart
+    # headline = the v_mad_u64_u32 our kernels execute (frac_actual).  The reference algorithm's work
+    # (its 254-bit Order*Q subgroup check included, which this path replaces by three psi maps on the
+    # line chain's final point) is reported only as a work ratio, not as a roofline fraction
+    k_prof = sum(v.get("avg_ms") or 0.0 for v in kk.values())
     roof = {"bound": "valu", "unit": "TMAC/s", "achieved": round(act / 1e12, 3) if act else None,
             "peak": round(PEAK_MAC / 1e12, 3), "frac": round(act / PEAK_MAC, 4) if act else None,
             "frac_actual": round(act / PEAK_MAC, 4) if act else None,
-            "achieved_reference_equiv": round(ref_ach / 1e12, 3), "frac_reference_equiv": round(ref_ach / PEAK_MAC, 4),
+            **(clock_fracs(oc["mac_equiv"] * nloc, {"avg_ms": k_prof,
+                                                    "profiled_clock_ghz": kk["k_bn_miller"].get("profiled_clock_ghz")},
+                           PEAK_MAC) if oc and k_prof and nloc == N_CHECKS else {}),
+            "reference_work_ratio": round(FP_MULS_PER_CHECK_REF * MACS_PER_FP_MUL / oc["mac_equiv"], 3) if oc else None,
             "mac_equiv_per_check_reference": FP_MULS_PER_CHECK_REF * MACS_PER_FP_MUL,
             "mac_equiv_per_check_actual": oc["mac_equiv"] if oc else None,
             "fp_products_per_check_actual": oc.get("fp_products") if oc else None,
