@@ -854,8 +854,21 @@ enum : uint8_t {
     FE_LDA,    // A = ws[slot]
     FE_STX,    // ws[slot] = X
     FE_LDFV,   // A = the next Miller-lane value of the check (prologue; not in the program)
+    FE_CSQR_LDA,  // X = X^2 while A = ws[slot] is fetched (the loads issue before the squaring)
 };
-static_assert(BN_FINAL_SLOTS == 4, "the program uses slots 0..3");
+// BN_FE_W4 = 1: the exponentiations by u use width-4 signed digits of u (13 products below the leading
+// digit instead of the NAF's 23, plus 3 for the odd powers a^3, a^5, a^7).  The odd powers go to
+// workspace slots 4..7; each digit's power is fetched into A during the squaring after the previous
+// product, so its load latency hides under that squaring.  0: the NAF (A = a throughout).
+#ifndef BN_FE_W4
+#define BN_FE_W4 1
+#endif
+// width-4 digits of u below bit 62 (u = 2^62 + sum d_i 2^i, constants.go:17): bit i of U_W4_NZ set
+// where d_i != 0, of U_W4_NEG where d_i < 0; (|d_i| - 1) / 2 = U_W4_I0 bit + 2 U_W4_I1 bit
+constexpr uint64_t U_W4_NZ = 0x108844442110211ULL, U_W4_NEG = 0x8004400010010ULL;
+constexpr uint64_t U_W4_I0 = 0x8800400110000ULL, U_W4_I1 = 0x100044002110200ULL;
+static_assert(BN_FINAL_SLOTS == 8, "the program uses slots 0..3, the odd powers 4..7");
+constexpr int FE_T0 = 4;  // slots FE_T0 + k: a^(2k+1) of the exponentiation in progress
 constexpr int FE_MAXOPS = 384;
 struct FeProg {
     uint8_t op[FE_MAXOPS];
@@ -867,12 +880,38 @@ struct FeBuild {
     // X = A^u (gfp12.go:113-127 on the NAF of u, constants.go:17; a^-1 = conj(a) in the cyclotomic
     // subgroup); A unchanged
     constexpr void exp_u() {
+#if BN_FE_W4
+        e(FE_AX), e(FE_STX, FE_T0), e(FE_CSQR), e(FE_XA), e(FE_LDX, FE_T0);  // A = a^2, X = a
+        for (int k = 1; k < 4; k++) e(FE_MUL), e(FE_STX, FE_T0 + k);         // a^3, a^5, a^7
+        e(FE_LDX, FE_T0);                                                     // the leading digit
+        int held = -1;  // the power A holds (-1: a^2, no longer needed)
+        bool free = true;  // A may be overwritten (its last product is done)
+        for (int i = 61; i >= 0; i--) {
+            // the next digit's power, fetched during the first squaring after the previous product
+            int nxt = -1;
+            for (int j = i; j >= 0 && nxt < 0; j--)
+                if ((U_W4_NZ >> j) & 1) nxt = (int)((U_W4_I0 >> j) & 1) | (int)(((U_W4_I1 >> j) & 1) << 1);
+            if (free && nxt >= 0 && nxt != held) {
+                e(FE_CSQR_LDA, FE_T0 + nxt);
+                held = nxt;
+            } else {
+                e(FE_CSQR);
+            }
+            free = true;
+            if ((U_W4_NZ >> i) & 1) {
+                e((U_W4_NEG >> i) & 1 ? FE_MULC : FE_MUL);
+                free = true;
+            }
+        }
+        e(FE_LDA, FE_T0);  // A = a again
+#else
         e(FE_AX);  // the leading digit (bit 62)
         for (int i = 61; i >= 0; i--) {
             e(FE_CSQR);
             if ((U_NAF_POS >> i) & 1) e(FE_MUL);
             if ((U_NAF_NEG >> i) & 1) e(FE_MULC);
         }
+#endif
     }
     constexpr FeProg build() {
         // easy part: X = in
@@ -941,17 +980,40 @@ GSV_DI fp6 lds_fp6(const uint32_t* lds, int half) {
     return e;
 }
 GSV_DI fp12 lds_fp12(const uint32_t* lds) { return fp12{lds_fp6(lds, 0), lds_fp6(lds, 1)}; }
+// A = ws[slot] straight from HBM into LDS (global_load_lds_dword: word q of every lane lands at
+// lds_base[q * 64 + lane], the [word][lane] layout A has), no VGPRs on the way; the data is there after
+// fe_lds_wait()
+GSV_DI void lds_fetch(uint32_t* lds_base, const uint32_t* __restrict__ ws, uint32_t n, uint32_t c, int slot) {
+    // saddr form: the workspace base in SGPRs, a 32-bit VGPR byte offset per word (< 2^32: the
+    // workspace is BN_FINAL_SLOTS x 432 bytes per check); M0 = the word's LDS row
+    const uint32_t off = ((uint32_t)slot * 108u * n + c) * 4u;
+    const uint32_t row = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)lds_base;
+#pragma unroll
+    for (int q = 0; q < 108; q++)
+        asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(off + (uint32_t)q * n * 4u), "s"(ws),
+                     "s"(row + (uint32_t)q * 256u)
+                     : "memory", "m0");
+}
+GSV_DI void fe_lds_wait() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15 left open)
+    asm volatile("" ::: "memory");
+}
 GSV_DI void lds_put(uint32_t* lds, const fp12& e) {
     const uint32_t* w = (const uint32_t*)&e;
 #pragma unroll
     for (int q = 0; q < 108; q++) lds[q * 64] = w[q];
 }
-// A.x of the operand, conjugated (negated) for FE_MULC
-GSV_DI fp6 lds_ax(const uint32_t* lds, bool conj) {
-    fp6 ax = lds_fp6(lds, 0);
-    if (conj) ax = fp6_store(fp6_neg(ax));
-    return ax;
-}
+// the operand's halves from LDS; x conjugated (negated) for FE_MULC
+struct FeOperand {
+    const uint32_t* lds;
+    bool conj;
+    GSV_DI fp6 x() const {
+        fp6 v = lds_fp6(lds, 0);
+        if (conj) v = fp6_store(fp6_neg(v));
+        return v;
+    }
+    GSV_DI fp6 y() const { return lds_fp6(lds, 1); }
+};
 // an F_p element below 2^256 (limbs normalised, value < 3p) packed into eight words and back: the
 // 29-bit limbs are the value's base-2^29 digits, so the round trip is exact
 GSV_DI void fq_pack_lds(uint32_t* lds, const fqm<1, 3>& a) {
@@ -987,9 +1049,9 @@ GSV_DI fqm<1, 3> fq_unpack_lds(const uint32_t* lds) {
 // A's 108: 156 words per lane, 39 KB per workgroup) and v1 and X.x + X.y take X's registers — so each
 // product runs with only one other F_p^6 value live beside it, and nothing spills.
 constexpr int FE_LDS_V0 = 108;  // word offset of the packed v0 in the lane's LDS column
-GSV_DI void fp12_mul_lds(fp12& X, uint32_t* lds, bool conj) {
+GSV_DI void fp12_mul_lds(fp12& X, uint32_t* lds, const FeOperand& B) {
     {
-        auto v0 = fp6_mul(X.x, lds_ax(lds, conj));
+        auto v0 = fp6_mul(X.x, B.x());
         fq_pack_lds(lds + (FE_LDS_V0 + 0) * 64, fq_reduce(v0.x.x));
         fq_pack_lds(lds + (FE_LDS_V0 + 8) * 64, fq_reduce(v0.x.y));
         fq_pack_lds(lds + (FE_LDS_V0 + 16) * 64, fq_reduce(v0.y.x));
@@ -999,9 +1061,9 @@ GSV_DI void fp12_mul_lds(fp12& X, uint32_t* lds, bool conj) {
     }
     __builtin_amdgcn_sched_barrier(0);
     X.x = fp6_store(fp6_add(X.x, X.y));
-    X.y = fp6_store(fp6_mul(X.y, lds_fp6(lds, 1)));  // v1
+    X.y = fp6_store(fp6_mul(X.y, B.y()));  // v1
     __builtin_amdgcn_sched_barrier(0);
-    fp6 v2 = fp6_store(fp6_mul(X.x, fp6_add(lds_ax(lds, conj), lds_fp6(lds, 1))));
+    fp6 v2 = fp6_store(fp6_mul(X.x, fp6_add(B.x(), B.y())));
     __builtin_amdgcn_sched_barrier(0);
     using e3 = fp2m<1, 3>;
     fp6t<e3> v0{e3{fq_unpack_lds(lds + (FE_LDS_V0 + 0) * 64), fq_unpack_lds(lds + (FE_LDS_V0 + 8) * 64)},
@@ -1011,9 +1073,9 @@ GSV_DI void fp12_mul_lds(fp12& X, uint32_t* lds, bool conj) {
     X.y = fp6_store(fp6_add(X.y, fp6_mul_tau(v0)));
 }
 // the three-lane form of fp12_mul_i: role 0 X.x A.x, role 1 X.y A.y, role 2 (X.x + X.y)(A.x + A.y)
-GSV_DI void fp12_mul3_lds(fp12& X, const uint32_t* lds, bool conj, int role, int base) {
+GSV_DI void fp12_mul3_lds(fp12& X, const FeOperand& B, int role, int base) {
     fp6 l = role == 0 ? X.x : role == 1 ? X.y : fp6_store(fp6_add(X.x, X.y));
-    fp6 ax = lds_ax(lds, conj), ay = lds_fp6(lds, 1);
+    fp6 ax = B.x(), ay = B.y();
     fp6 r = role == 0 ? ax : role == 1 ? ay : fp6_store(fp6_add(ax, ay));
     fp6 prod = fp6_store(fp6_mul(l, r)), v[3];
     gather3(v, prod, base);
@@ -1075,13 +1137,18 @@ GSV_DI fp12 final_exp_run(fp12 X, const FinalArgs& fa, uint32_t* lds_base, uint3
         if (k == FE_END) break;
         const FeLane<COOP> ln;
         uint32_t* lds = lds_base + ln.lane;
+        if (k != FE_CSQR && k != FE_CSQR_LDA) fe_lds_wait();  // an A fetched by an earlier op has landed
         switch (k) {
         case FE_MUL:
-        case FE_MULC:
-            if constexpr (COOP) fp12_mul3_lds(X, lds, k == FE_MULC, ln.role(), ln.base());
-            else fp12_mul_lds(X, lds, k == FE_MULC);
+        case FE_MULC: {
+            const FeOperand B{lds, k == FE_MULC};
+            if constexpr (COOP) fp12_mul3_lds(X, B, ln.role(), ln.base());
+            else fp12_mul_lds(X, lds, B);
             break;
+        }
         case FE_CSQR:
+        case FE_CSQR_LDA: {
+            if (k == FE_CSQR_LDA) lds_fetch(lds_base, fa.ws, fa.nchecks, ln.check(), (int)slot);
             if constexpr (COOP) {
                 fp12 m;
                 fp12_cyclo_sqr3_i(&m, X, ln.role(), ln.base());
@@ -1090,6 +1157,7 @@ GSV_DI fp12 final_exp_run(fp12 X, const FinalArgs& fa, uint32_t* lds_base, uint3
                 X = fp12_cyclo_sqr_i(X);
             }
             break;
+        }
         case FE_FROB: X = fp12_frob_i(X); break;
         case FE_FROB2: X = fp12_frob_p2_i(X); break;
         case FE_CONJ: X = fp12_conj(X); break;
@@ -1103,7 +1171,7 @@ GSV_DI fp12 final_exp_run(fp12 X, const FinalArgs& fa, uint32_t* lds_base, uint3
             break;
         }
         case FE_LDX: X = ws_load(fa.ws, fa.nchecks, ln.check(), (int)slot); break;
-        case FE_LDA: lds_put(lds, ws_load(fa.ws, fa.nchecks, ln.check(), (int)slot)); break;
+        case FE_LDA: lds_fetch(lds_base, fa.ws, fa.nchecks, ln.check(), (int)slot); break;
         case FE_STX: ws_store(fa.ws, fa.nchecks, ln.check(), (int)slot, X); break;
         case FE_LDFV: lds_put(lds, fv_extra(fa, ln.check(), pc >> 1)); break;
         default: break;

@@ -834,11 +834,29 @@ __global__ __launch_bounds__(256) GSV_LEVEL_ATTR void k_chunk_level(const PNode*
 }
 
 // ---------------------------------------------------------------- fused top of the trie
+#ifndef GSV_TOP_PRIO_DEFAULT
+#define GSV_TOP_PRIO_DEFAULT 1
+#endif
 struct TopLevels {
     int h0, h1;  // heights h0..h1 (inclusive), index h - 1 below
     int hb[TOP_MAX_H], he[TOP_MAX_H], gb[TOP_MAX_H], ge[TOP_MAX_H];
     uint32_t gen_lane;  // bit h - 1: that height's generic nodes one per lane (throughput form)
+    int prio;           // nonzero: the top's waves run at the highest wave priority (s_setprio 3)
 };
+// The fused top is a short dependent chain (~17 permutations from height 3 to the root) that usually
+// runs BESIDE bulk work: the next batch's bottom level (pipelined chunk roots) or k_notary_tx (the
+// notary forks its chunk roots onto a side stream).  At equal priority the SQ's arbiter shares each
+// SIMD's issue slots among all resident waves, so the top's chain advances at a fraction of its speed
+// and its workgroups hold their CUs' wave slots and LDS for the whole overlap.  At priority 3 its
+// waves issue first: the chain finishes in about its solo time and hands the slots back.
+// GSV_TOP_PRIO = 0 / 1 overrides the default (A/B).
+inline int top_prio() {
+    static int p = [] {
+        const char* e = getenv("GSV_TOP_PRIO");
+        return e ? atoi(e) : GSV_TOP_PRIO_DEFAULT;
+    }();
+    return p;
+}
 constexpr uint32_t TOP_MAX_BODIES = 256;  // one fused-top workgroup per CU at most
 #ifndef GSV_TOP_HFULL_THREADS
 #define GSV_TOP_HFULL_THREADS 256
@@ -861,6 +879,7 @@ __global__ __launch_bounds__(TOP_BLOCK) void k_chunk_top(const PNode* __restrict
                                                          const PChild* __restrict__ children, TopLevels tl,
                                                          BodyBatch bb) {
     __shared__ uint64_t gbuf[TOP_GROUPS * MSG_STRIDE / 8];
+    if (tl.prio) __builtin_amdgcn_s_setprio(3);
     uint32_t body = blockIdx.x;
     int tid = threadIdx.x, grp = tid >> 5;
     uint8_t* m = (uint8_t*)gbuf + grp * MSG_STRIDE;
@@ -952,6 +971,7 @@ static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipSt
         TopLevels tl{};
         tl.h0 = top_h;
         tl.h1 = p.height;
+        tl.prio = top_prio();
         for (int h = 1; h <= p.height; h++) {
             tl.hb[h - 1] = p.lvl_hfull_begin[h - 1];
             tl.he[h - 1] = p.lvl_hfull_end[h - 1];

@@ -70,7 +70,7 @@ struct BnConcurrent {
 // lines[91 * 54][npairs], lstat[nlanes], fv[108][nlanes] words, fws[BN_FINAL_SLOTS * 108][nchecks]
 // words (the final exponentiation's values that outlive its registers); maxl = the most lanes any
 // check has.  final3: the final exponentiation runs on three cooperating lanes per check (small batches)
-constexpr int BN_FINAL_SLOTS = 4;
+constexpr int BN_FINAL_SLOTS = 8;
 hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src, uint32_t npairs,
                                 const uint32_t* d_lane_first, const uint32_t* d_pidx, uint32_t nlanes,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,

@@ -167,10 +167,16 @@ def _synth_scalar(oracle, seed, i, tag):
 
 
 def test_synth_checks_match_oracle(ctx, oracle):
-    """configs[4] generator (gsv_bn256_synth_checks_dev): bytes equal the oracle's G1/G2 scalar
-    multiples of the same Keccak-derived scalars, and every check's verdict matches both the
-    oracle and the generator's expected verdict."""
+    """configs[4] generator (gsv_bn256_synth_checks_dev): bytes equal the CPU rebuild from the oracle's
+    G1/G2 scalar multiples of the same Keccak-derived scalars (tests/golden/make_golden.py
+    configs4_inputs), for every check class (true, false, infinity pairs, G2 outside the subgroup with
+    and without an infinite G1, off the twist, coordinate == p), and every check's verdict matches both
+    the oracle and the generator's expected verdict."""
+    import os
+    import sys
     import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_golden import configs4_inputs
     n, seed = 1024, 77
     out = torch.empty((n, 768), dtype=torch.uint8, device="cuda")
     exp = torch.empty((n,), dtype=torch.uint8, device="cuda")
@@ -178,21 +184,13 @@ def test_synth_checks_match_oracle(ctx, oracle):
     torch.cuda.synchronize()
     h = out.cpu().numpy()
     e = exp.cpu().numpy()
-    P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
-    for c in [0, 1, 7, 1023]:
-        a, b, cc, d = (_synth_scalar(oracle, seed, c, t) for t in (0x61, 0x62, 0x63, 0x64))
-        d1 = d + 1 if c % 8 == 7 else d  # the false checks use -(d+1)P in the last pair
-        want = (oracle.bn256_g1_mul(a) + oracle.bn256_g2_mul(b) + oracle.bn256_g1_mul(-b % R) +
-                oracle.bn256_g2_mul(a) + oracle.bn256_g1_mul(cc) + oracle.bn256_g2_mul(d) +
-                oracle.bn256_g1_mul(-d1 % R) + oracle.bn256_g2_mul(cc))
-        if c % 1024 == 1023:
-            want = want[:384] + P.to_bytes(32, "big") + want[416:]
-        assert bytes(h[c]) == want, c
-    for c in range(0, n, 37):
+    for c in [0, 1, 7, 100, 200, 300, 400, 500, 1023]:
+        assert bytes(h[c]) == configs4_inputs(c, seed), c
+    for c in list(range(0, n, 37)) + [100, 200, 300, 400, 500]:
         assert e[c] == _v(oracle, bytes(h[c])), c
     v = ctx.pairing_check_batch([bytes(r) for r in h])
     assert (v == e).all()
-    assert (e == 1).sum() and (e == 0).sum() and (e == 2).sum() == 1
+    assert (e == 1).sum() == 893 and (e == 0).sum() == 127 and (e == 2).sum() == 4
 
 
 def test_g2_subgroup_predicate_vs_oracle(ctx, oracle):
