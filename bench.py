@@ -800,7 +800,7 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     k_tot = (k_prep + k_mill + k_fin) / psteps
     oc = opcount("pairing_check")
     act = oc["mac_equiv"] * nloc / (k_tot * 1e-3) if oc else None
-    kk = {n: pmc(f"gsv::bn::{n}", "pmc_pairing.json") for n in ("k_bn_prepare", "k_bn_miller", "k_bn_final")}
+    kk = {n: pmc(f"gsv::bn::{n}", "pmc_pairing.json") for n in ("k_bn_lines", "k_bn_miller", "k_bn_final")}
     # headline = the v_mad_u64_u32 our kernels execute (frac_actual).  The reference algorithm's work
     # (its 254-bit Order*Q subgroup check included, which this path replaces by three psi maps on the
     # line chain's final point) is reported only as a work ratio, not as a roofline fraction

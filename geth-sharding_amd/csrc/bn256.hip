@@ -650,6 +650,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
         uint32_t j = pidx[q];
         if (pstat[j] == PS_OK) jv[m++] = j;
     }
+    // every lane walks the wave's largest pair count mw (a lane with fewer finite pairs, e.g. an
+    // infinity pair skipped, idles through the extra line products): the squarings at the step
+    // boundaries then stay wave-uniform instead of running once per distinct pair count
+    const int mw = __ballot(m >= 4) ? 4 : __ballot(m >= 3) ? 3 : __ballot(m >= 2) ? 2 : 1;
+    for (int t = m; t < 4; t++) jv[t] = jv[0];
     auto nl_of = [](int i) { return i == 0 || (((NAF_POS | NAF_NEG) >> (i - 1)) & 1ull) ? 2 : 1; };
     line cur = line_load(lines, npairs, jv[0], 0);
     int i = 64, q = 0, k = 0, li = 0;  // step i = 64..1 (the loop), 0 = the two Frobenius lines
@@ -659,7 +664,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
         if (nk >= nl_of(i)) {
             nk = 0;
             nq = q + 1;
-            if (nq >= m) {
+            if (nq >= mw) {
                 nq = 0;
                 nli = li + nl_of(i);
                 ni = i - 1;
@@ -668,7 +673,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
         bool more = ni >= 0;
         line nxt = cur;
         if (more) nxt = line_load(lines, npairs, jv[nq], nli + nk);
-        mul_line_i(f, cur);
+        if (q < m) mul_line_i(f, cur);
         if (!more) break;
         if (ni != i && ni != 0) f = fp12_sqr_i(f);
         cur = nxt;

@@ -835,7 +835,7 @@ __global__ __launch_bounds__(256) GSV_LEVEL_ATTR void k_chunk_level(const PNode*
 
 // ---------------------------------------------------------------- fused top of the trie
 #ifndef GSV_TOP_PRIO_DEFAULT
-#define GSV_TOP_PRIO_DEFAULT 1
+#define GSV_TOP_PRIO_DEFAULT 0
 #endif
 struct TopLevels {
     int h0, h1;  // heights h0..h1 (inclusive), index h - 1 below
@@ -849,7 +849,8 @@ struct TopLevels {
 // SIMD's issue slots among all resident waves, so the top's chain advances at a fraction of its speed
 // and its workgroups hold their CUs' wave slots and LDS for the whole overlap.  At priority 3 its
 // waves issue first: the chain finishes in about its solo time and hands the slots back.
-// GSV_TOP_PRIO = 0 / 1 overrides the default (A/B).
+// Measured within noise (r04: configs[2] 91.7 vs 91.8 GB/s, the notary leg 9,844 vs 9,843 shards/s,
+// 13 / 100 shards per step unchanged), so it is off by default; GSV_TOP_PRIO = 0 / 1 overrides.
 inline int top_prio() {
     static int p = [] {
         const char* e = getenv("GSV_TOP_PRIO");

@@ -825,8 +825,12 @@ bool bn_miller2(size_t nlanes, int cus, int depth) {
 // GSV_BN_LAYOUT_CONC, below about one wave per SIMD: the lines kernel at a one-wave register budget (no
 // spills), and in the BN_SUB_FROB = 0 build the curve / subgroup checks on a side stream beside it and
 // the Miller loop.  GSV_BN_CONC = 0/1 forces the choice (A/B timing).
+// In the default (BN_SUB_FROB) build the layout only picks the lines kernel at a one-wave register budget,
+// which has no spills; at 65,536 checks it takes the same time as the two-wave k_bn_prepare (7.27 vs
+// 7.26 ms, profiles/r04) without its 696 B/lane of spill traffic, so it is used at every size.
 bool bn_conc(size_t npairs, int cus) {
     if (const char* e = getenv("GSV_BN_CONC")) return atoi(e) != 0;
+    if (!gsv::bn256_layout_forks()) return true;
     return npairs <= (size_t)std::max(cus, 1) * 4 * 64 * 1;
 }
 // Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per

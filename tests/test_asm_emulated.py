@@ -83,6 +83,10 @@ class Machine:
                 res = (self.r64(a[1]) << int(a[2])) + self.r64(a[3])
                 assert res <= M64, f"64-bit overflow in {ln}"
                 self.w64(a[0], res)
+            elif op == "v_lshlrev_b32":
+                res = self.r32(a[2]) << int(a[1])
+                assert res <= M32, f"32-bit shift loses bits in {ln}"
+                self.w32(a[0], res)
             elif op == "v_and_b32_e32":
                 self.w32(a[0], int(a[1], 0) & self.r32(a[2]))
             elif op == "v_mov_b32":
@@ -140,17 +144,30 @@ def fe9_case(rng, ma, mb, extreme):
     return a, b
 
 
+OPND1 = {"r": 0, "a": 18, "b": 27, "k31264": 36, "k256": 37, "k977": 38, "c": 39, "d": 48}
+# the two column forms of tools/gen_fe9_asm.py (GSV_FE9_COLS 1 / 2) and their operand numbering
+FORMS = {1: (gen_fe9_asm.full_lines, OPND1), 2: (gen_fe9_asm.full_lines2, gen_fe9_asm.OPND2)}
+
+
+def fe9_lines(form, terms, addend=False):
+    gen, lay = FORMS[form]
+    return (gen(terms, addend), lay)
+
+
 def run_fe9(lines, a, b, c=None, d=None):
-    ops = {18 + i: a[i] for i in range(9)}
-    ops.update({27 + j: b[j] for j in range(9)})
+    lines, O = lines
+    ops = {O["a"] + i: a[i] for i in range(9)}
+    ops.update({O["b"] + j: b[j] for j in range(9)})
     if c is not None:
-        ops.update({39 + j: c[j] for j in range(9)})
+        ops.update({O["c"] + j: c[j] for j in range(9)})
     if d is not None:
-        ops.update({48 + j: d[j] for j in range(9)})
-    ops.update({36: 31264, 37: 256, 38: 977})
+        ops.update({O["d"] + j: d[j] for j in range(9)})
+    ops.update({O["k31264"]: 31264, O["k256"]: 256, O["k977"]: 977})
+    if "k8192" in O:
+        ops[O["k8192"]] = 8192
     m = Machine(ops)
     m.run(lines)
-    return [m.ops[i] for i in range(9)]
+    return [m.ops[O["r"] + i] for i in range(9)]
 
 
 def check_weak(r, want):
@@ -159,18 +176,20 @@ def check_weak(r, want):
 
 
 @pytest.mark.parametrize("ma,mb", [(1, 1), (1, 7), (7, 1), (2.64, 2.64), (2, 3.5)])
-def test_fe9_mul_asm(ma, mb):
+@pytest.mark.parametrize("form", [1, 2])
+def test_fe9_mul_asm(form, ma, mb):
     rng = random.Random(int(ma * 100 + mb))
-    lines = gen_fe9_asm.full_lines(gen_fe9_asm.MUL_TERMS)
+    lines = fe9_lines(form, gen_fe9_asm.MUL_TERMS)
     for it in range(150):
         a, b = fe9_case(rng, ma, mb, extreme=(it == 0))
         check_weak(run_fe9(lines, a, b), limbs_val(a) * limbs_val(b))
 
 
 @pytest.mark.parametrize("ma", [1, 2, 2.64])
-def test_fe9_sqr_asm(ma):
+@pytest.mark.parametrize("form", [1, 2])
+def test_fe9_sqr_asm(form, ma):
     rng = random.Random(int(ma * 100))
-    lines = gen_fe9_asm.full_lines(gen_fe9_asm.SQR_TERMS)
+    lines = fe9_lines(form, gen_fe9_asm.SQR_TERMS)
     for it in range(150):
         a, _ = fe9_case(rng, ma, 1, extreme=(it == 0))
         a2 = [x << 1 for x in a]
@@ -189,9 +208,10 @@ def addend_case(rng, extreme):
 
 
 @pytest.mark.parametrize("ma,mb", [(1.04, 1.04), (1, 3), (1.04, 4.16), (1, 7)])
-def test_fe9_mul_add_asm(ma, mb):
+@pytest.mark.parametrize("form", [1, 2])
+def test_fe9_mul_add_asm(form, ma, mb):
     rng = random.Random(int(ma * 1000 + mb))
-    lines = gen_fe9_asm.full_lines(gen_fe9_asm.MUL_TERMS, addend=True)
+    lines = fe9_lines(form, gen_fe9_asm.MUL_TERMS, addend=True)
     for it in range(150):
         a, b = fe9_case(rng, ma, mb, extreme=(it == 0))
         c = addend_case(rng, extreme=(it < 2))
@@ -199,9 +219,10 @@ def test_fe9_mul_add_asm(ma, mb):
 
 
 @pytest.mark.parametrize("ma", [1, 1.04, 2.64])
-def test_fe9_sqr_add_asm(ma):
+@pytest.mark.parametrize("form", [1, 2])
+def test_fe9_sqr_add_asm(form, ma):
     rng = random.Random(int(ma * 1000) + 7)
-    lines = gen_fe9_asm.full_lines(gen_fe9_asm.SQR_TERMS, addend=True)
+    lines = fe9_lines(form, gen_fe9_asm.SQR_TERMS, addend=True)
     for it in range(150):
         a, _ = fe9_case(rng, ma, 1, extreme=(it == 0))
         a2 = [x << 1 for x in a]
@@ -210,11 +231,12 @@ def test_fe9_sqr_add_asm(ma):
 
 
 @pytest.mark.parametrize("m", [(1.04, 3.04, 1.04, 3), (1, 3.5, 1, 3.5), (1.04, 1.04, 2.64, 2.2)])
-def test_fe9_dot_asm(m):
+@pytest.mark.parametrize("form", [1, 2])
+def test_fe9_dot_asm(form, m):
     """a*b + c*d with one reduction at m_a m_b + m_c m_d <= 7 (the mixed add's Y3: rr (V - X3) + Y1 (-2J))"""
     ma, mb, mc, md = m
     rng = random.Random(int(sum(m) * 1000))
-    lines = gen_fe9_asm.full_lines(gen_fe9_asm.DOT_TERMS)
+    lines = fe9_lines(form, gen_fe9_asm.DOT_TERMS)
     for it in range(150):
         a, b = fe9_case(rng, ma, mb, extreme=(it == 0))
         c, d = fe9_case(rng, mc, md, extreme=(it == 0))
@@ -228,7 +250,8 @@ def _q_consts():
     return {m + 1: [int(x.strip().rstrip("u"), 16) for x in rows[m].strip().strip("{},").split(",")] for m in range(7)}
 
 
-def test_fe9_dot_asm_at_the_mixed_add_operands():
+@pytest.mark.parametrize("form", [1, 2])
+def test_fe9_dot_asm_at_the_mixed_add_operands(form):
     """the operands fe9_dot actually gets in gej9_add_ge_core, at their largest limbs: rr and Y1 are
     product outputs (limb 2 up to 2^29 + 2^24), V - X3 = V + (Q_1 - X3), -2J = Q_2 - J - J (limb 8
     near 2^30, far above a product output's 2^24)"""
@@ -238,7 +261,7 @@ def test_fe9_dot_asm_at_the_mixed_add_operands():
     prod[8] = (1 << 24) - 1
     t = [prod[i] + Q[1][i] for i in range(9)]      # V - X3 with X3 = 0
     w = list(Q[2])                                 # -2J with J = 0
-    lines = gen_fe9_asm.full_lines(gen_fe9_asm.DOT_TERMS)
+    lines = fe9_lines(form, gen_fe9_asm.DOT_TERMS)
     check_weak(run_fe9(lines, prod, t, prod, w), limbs_val(prod) * limbs_val(t) + limbs_val(prod) * limbs_val(w))
     rng = random.Random(99)
     for _ in range(200):

@@ -128,17 +128,135 @@ def full_lines(terms_of_column, addend=False):
     return L
 
 
+
+# ---------------------------------------------------------------------------- column form 2
+# Operand numbering of the form-2 statements (the emulator test reads it): %0..%8 r, %9 the dead
+# carry-out SGPR pair, then a, b, the three SGPR constants, c, d.
+OPND2 = {"r": 0, "sd": 9, "a": 10, "b": 19, "k31264": 28, "k256": 29, "k977": 30, "k8192": 31, "c": 32, "d": 41}
+PAIR2 = {k: f"v[{6 + 2 * (k - 10)}:{7 + 2 * (k - 10)}]" for k in range(10, 17)}  # columns 10..16
+
+
+def full_lines2(terms_of_column, addend=False):
+    """Form 2: the high columns 9..16 are never masked or shifted.  Column 9 accumulates in
+    C = v[2:3] (from column 8's C >> 29, as form 1); column k = 10..16 in its own fixed pair P_k
+    (v[6:7] .. v[18:19]) starting from 8 * hi(P_{k-1}) (one multiply-add, in place of the 64-bit shift)
+    and keeps its 32-bit low word o_k = C_k mod 2^32 unmasked: sum_k o_k 2^(29 k) is still the product,
+    because the carry into column k is floor(C_{k-1} / 2^32) at weight 2^(29 (k-1) + 32) = 8 * 2^(29 k).
+    The reduction reads o_9..o_16 through multiply-adds (31264 o, 256 o < 2^47), so an unmasked 32-bit
+    limb costs nothing there; o17 = 8 hi(P_16) < 2^23 is a 32-bit value (one shift), and
+    T = (c >> 24) + o17 2^13 one multiply-add.  Per product 8 masks, a 64-bit shift, a 64-bit
+    shift-add and a u24 multiply-add fewer than form 1."""
+    O = OPND2
+    opnd = lambda x: f"%{O['a'] + x}" if x < 9 else (f"%{O['b'] + x - 9}" if x < 18 else f"%{O['c'] + x - 18}")
+    cj = lambda j: f"%{O['c'] + j}"
+    r = lambda k: f"%{O['r'] + k}"
+    C, c0, c1 = "v[2:3]", "v2", "v3"
+    D, d0, d1 = "v[4:5]", "v4", "v5"
+    lo = lambda k: "v2" if k == 9 else f"v{6 + 2 * (k - 10)}"
+    hi = lambda k: "v3" if k == 9 else f"v{7 + 2 * (k - 10)}"
+    K31264, K256, K977, SD = f"%{O['k31264']}", f"%{O['k256']}", f"%{O['k977']}", f"%{O['sd']}"
+    K8192 = f"%{O['k8192']}"  # VOP3 takes no literal on gfx950: 2^13 from an SGPR
+    L = []
+    for k in range(17):
+        if k <= 9:
+            acc, first = C, True
+            if k > 0:
+                L.append(f"v_lshrrev_b64 {C}, 29, {C}")
+                first = False
+        else:
+            acc = PAIR2[k]
+            L.append(f"v_mad_u64_u32 {acc}, {SD}, {hi(k - 1)}, 8, 0")  # 8 * floor(C_{k-1} / 2^32)
+            first = False
+        for (x, y) in terms_of_column(k):
+            L.append(f"v_mad_u64_u32 {acc}, {SD}, {opnd(x)}, {opnd(y)}, {'0' if first else acc}")
+            first = False
+        if k <= 8:
+            L.append(f"v_and_b32_e32 {r(k)}, 0x1fffffff, {c0}")
+    L.append(f"v_lshlrev_b32 {c1}, 3, {hi(16)}")          # o17 = 8 hi(P_16) (C's high word is free)
+    # limbs 0..7: c = o_j + carry + 31264 o_{j+9} + 256 o_{j+8}
+    L.append(f"v_mov_b32 {d1}, 0")
+    if addend:
+        L.append(f"v_add_u32 {d0}, {r(0)}, {cj(0)}")
+    else:
+        L.append(f"v_mov_b32 {d0}, {r(0)}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {lo(9)}, {K31264}, {D}")
+    L.append(f"v_and_b32_e32 {r(0)}, 0x1fffffff, {d0}")
+    for j in range(1, 8):
+        L.append(f"v_lshrrev_b64 {D}, 29, {D}")           # carry < 2^19: the high word is 0
+        if addend:
+            L.append(f"v_add3_u32 {d0}, {d0}, {r(j)}, {cj(j)}")
+        else:
+            L.append(f"v_add_u32 {d0}, {d0}, {r(j)}")
+        L.append(f"v_mad_u64_u32 {D}, {SD}, {lo(j + 9)}, {K31264}, {D}")
+        L.append(f"v_mad_u64_u32 {D}, {SD}, {lo(j + 8)}, {K256}, {D}")
+        L.append(f"v_and_b32_e32 {r(j)}, 0x1fffffff, {d0}")
+    # limb 8: o_8 + carry + 31264 o17 + 256 o_16; 24 bits stay, the rest (units of 2^256) is T
+    L.append(f"v_lshrrev_b64 {D}, 29, {D}")
+    if addend:
+        L.append(f"v_add3_u32 {d0}, {d0}, {r(8)}, {cj(8)}")
+    else:
+        L.append(f"v_add_u32 {d0}, {d0}, {r(8)}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {c1}, {K31264}, {D}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {lo(16)}, {K256}, {D}")
+    L.append(f"v_and_b32_e32 {r(8)}, 0xffffff, {d0}")
+    L.append(f"v_lshrrev_b64 {D}, 24, {D}")
+    T, t0, t1 = "v[6:7]", "v6", "v7"                      # P_10 is dead by now
+    L.append(f"v_mad_u64_u32 {T}, {SD}, {c1}, {K8192}, {D}")  # T = (c >> 24) + o17 2^13 < 2^37
+    # 2^256 == 2^32 + 977: limb 0 += 977 T, limb 1 += 8 T (+ carries), limb 2 += carry
+    L.append(f"v_mov_b32 {d1}, 0")
+    L.append(f"v_mov_b32 {d0}, {r(0)}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {t0}, {K977}, {D}")
+    L.append(f"v_mad_u32_u24 {d1}, {t1}, {K977}, {d1}")
+    L.append(f"v_and_b32_e32 {r(0)}, 0x1fffffff, {d0}")
+    L.append(f"v_lshrrev_b64 {D}, 29, {D}")
+    L.append(f"v_lshl_add_u64 {D}, {T}, 3, {D}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {r(1)}, 1, {D}")
+    L.append(f"v_and_b32_e32 {r(1)}, 0x1fffffff, {d0}")
+    L.append(f"v_alignbit_b32 {t0}, {d1}, {d0}, 29")
+    L.append(f"v_add_u32 {r(2)}, {r(2)}, {t0}")
+    return L
+
+
+def full2(name, doc, terms_of_column, addend=False, dot=False):
+    L = full_lines2(terms_of_column, addend)
+    outs = ", ".join([f'"=&v"(r[{i}])' for i in range(9)] + ['"=&s"(sd)'])
+    ins = ", ".join([f'"v"(a[{i}])' for i in range(9)] + [f'"v"(b[{j}])' for j in range(9)] +
+                    ['"s"(k31264)', '"s"(k256)', '"s"(k977)', '"s"(k8192)'] +
+                    ([f'"v"(c[{j}])' for j in range(9)] if addend or dot else []) +
+                    ([f'"v"(d[{j}])' for j in range(9)] if dot else []))
+    body = "\\n\\t".join(L)
+    clob = ", ".join(f'"v{i}"' for i in range(2, 20))
+    return [f"// {doc}",
+            f"__device__ __forceinline__ void {name}(uint32_t r[9], const uint32_t a[9], const uint32_t b[9]"
+            + (", const uint32_t c[9]" if addend or dot else "") + (", const uint32_t d[9]" if dot else "") + ") {",
+            "    uint64_t sd;",
+            "    uint32_t k31264 = 31264u, k256 = 256u, k977 = 977u, k8192 = 8192u;",
+            f'    asm("{body}"',
+            f"        : {outs}",
+            f"        : {ins}",
+            f"        : {clob});",
+            "}"]
+
 def main():
     out = ["// GENERATED by tools/gen_fe9_asm.py — do not edit by hand.",
            "// Column products of secp256k1_fe9.cuh as single inline-asm statements (see the generator's",
-           "// docstring for why).  c[k] = column k of a*b plus the carry of column k-1 (c[k-1] >> 29).",
-           "#pragma once", "#include <stdint.h>", "namespace gsv {"]
-    out += full("fe9_mul_full", "r = a * b mod p, weakly normalised (fe9_mul's contract)", MUL_TERMS)
-    out += full("fe9_sqr_full", "r = a^2 mod p with b = 2a limb-wise (fe9_sqr's contract)", SQR_TERMS)
-    out += full("fe9_mul_add_full", "r = a * b + c mod p, c limbs < 2^31 (fe9_mul_add's contract)", MUL_TERMS, True)
-    out += full("fe9_sqr_add_full", "r = a^2 + c mod p with b = 2a limb-wise, c limbs < 2^31 (fe9_sqr_add's contract)",
-                SQR_TERMS, True)
-    out += full("fe9_dot_full", "r = a * b + c * d mod p, one reduction (fe9_dot's contract)", DOT_TERMS, dot=True)
+           "// docstring for why).  GSV_FE9_COLS selects the column form: 2 (default) keeps the high columns",
+           "// 9..16 unmasked in fixed register pairs (full_lines2), 1 masks and shifts every column.",
+           "#pragma once", "#include <stdint.h>", "#ifndef GSV_FE9_COLS", "#define GSV_FE9_COLS 2", "#endif",
+           "namespace gsv {"]
+    specs = [("fe9_mul_full", "r = a * b mod p, weakly normalised (fe9_mul's contract)", MUL_TERMS, False, False),
+             ("fe9_sqr_full", "r = a^2 mod p with b = 2a limb-wise (fe9_sqr's contract)", SQR_TERMS, False, False),
+             ("fe9_mul_add_full", "r = a * b + c mod p, c limbs < 2^31 (fe9_mul_add's contract)", MUL_TERMS, True, False),
+             ("fe9_sqr_add_full", "r = a^2 + c mod p with b = 2a limb-wise, c limbs < 2^31 (fe9_sqr_add's contract)",
+              SQR_TERMS, True, False),
+             ("fe9_dot_full", "r = a * b + c * d mod p, one reduction (fe9_dot's contract)", DOT_TERMS, False, True)]
+    out.append("#if GSV_FE9_COLS == 1")
+    for name, doc, terms, add, dot in specs:
+        out += full(name, doc, terms, add, dot)
+    out.append("#else")
+    for name, doc, terms, add, dot in specs:
+        out += full2(name, doc, terms, add, dot)
+    out.append("#endif")
     out.append("}  // namespace gsv")
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")

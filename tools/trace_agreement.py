@@ -14,7 +14,7 @@ LEGS = {  # leg: (kernel name prefix in the trace, how to read the bench's HIP-e
     "ecrecover": ("gsv::k_ecrecover", lambda d: d["roofline"]["kernel_avg_ms"]),
     "chunk_root": ("void gsv::k_chunk_level<true>", lambda d: d["chunk_root"]["bottom_kernel_avg_ms"]),
     "keccak": ("gsv::k_keccak256", lambda d: d["collation_extras"]["keccak256"]["roofline"]["kernel_avg_ms"]),
-    "pairing:prepare": ("gsv::bn::k_bn_prepare", lambda d: d["bn256_pairing"]["prepare_kernel_ms"]),
+    "pairing:prepare": ("gsv::bn::k_bn_lines", lambda d: d["bn256_pairing"]["prepare_kernel_ms"]),
     "pairing:miller": ("gsv::bn::k_bn_miller", lambda d: d["bn256_pairing"]["miller_kernel_ms"]),
     "pairing:final": ("gsv::bn::k_bn_final", lambda d: d["bn256_pairing"]["final_exp_kernel_ms"]),
 }

@@ -29,7 +29,7 @@ def ov(tail, bulk):
             cov += b - max(a, last)
             last = b
     return len(T), tot / 1e3 / max(len(T), 1), cov / max(tot, 1)
-for tail, bulk in (("k_chunk_top", "k_chunk_level<true>"), ("k_bn_miller", "k_bn_prepare"), ("k_bn_final", "k_bn_prepare")):
+for tail, bulk in (("k_chunk_top", "k_chunk_level<true>"), ("k_bn_miller", "k_bn_lines"), ("k_bn_final", "k_bn_lines")):
     n, avg, frac = ov(tail, bulk)
     print(f"{tail:14s} dispatches {n:3d}  avg {avg:9.1f} us  overlapped by {bulk}: {100 * frac:5.1f} % of its time")
 PY
