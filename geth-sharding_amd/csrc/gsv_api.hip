@@ -939,11 +939,17 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.o_clane = L.add((n + 1) * 4);
     s.o_cbad = L.add(n);
     s.o_pstat = L.add(np + 1);
-    s.o_lines = L.add(np * 91 * 54 * 4 + 4);  // the pairs' Miller-loop lines (bn256.hip BN_NLINES)
+    // the pairs' Miller-loop lines (bn256.hip BN_NLINES).
+    // The final exponentiation's workspace (BN_FINAL_SLOTS F_p^12 values per check) reuses the region:
+    // the lines are dead once the Miller kernel, which precedes k_bn_final on the run's stream, is done.
+    // (a separate region measured the same, r04)
+    const size_t lines_bytes = np * 91 * 54 * 4;
+    const size_t fws_bytes = n * 108 * 4 * gsv::BN_FINAL_SLOTS;
+    s.o_lines = L.add(std::max(lines_bytes, fws_bytes) + 4);
     s.o_lstat = L.add(s.nl + 1);
     s.o_luse = L.add(np + 1);
     s.o_fv = L.add(s.nl * 108 * 4 + 4);
-    s.o_fws = L.add(n * 108 * 4 * gsv::BN_FINAL_SLOTS + 4);  // the final exponentiation's F_p^12 values
+    s.o_fws = s.o_lines;
     s.stage(s.o_src, pair_src.data(), np);
     s.stage(s.o_pidx, pidx.data(), np);
     s.stage(s.o_lfirst, lane_first.data(), lane_first.size());
@@ -991,7 +997,9 @@ int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verd
         conc = gsv::BnConcurrent{s.side[s.cur], s.efork[s.cur], s.ejoin[s.cur], s.at<uint8_t>(s.o_luse)};
         pc = &conc;
     }
-    int layout = pc ? s.layout : (s.layout & ~gsv::GSV_BN_LAYOUT_CONC);
+    // without a side stream the concurrent layout can only keep its kernel choice (the one-wave lines
+    // kernel), which is all it is in the default build (bn256_layout_forks() false)
+    int layout = (pc || !gsv::bn256_layout_forks()) ? s.layout : (s.layout & ~gsv::GSV_BN_LAYOUT_CONC);
     return hip_err(gsv::launch_bn256_pairing(
         d_in, s.at<uint64_t>(s.o_src), (uint32_t)s.np, s.at<uint32_t>(s.o_lfirst), s.at<uint32_t>(s.o_pidx),
         (uint32_t)s.nl, s.at<uint32_t>(s.o_clane), s.at<uint8_t>(s.o_cbad), (uint32_t)s.nchecks,
