@@ -68,7 +68,7 @@ VALU_ISSUE_PEAK = 0.5
 PEAK_LANE_OPS = SIMDS * 64 * VALU_ISSUE_PEAK * CLOCK          # 7.86e13 full-rate 32-bit lane-ops/s
 PEAK_MAC = SIMDS * 16 * CLOCK                                 # 3.93e13 v_mad_u64_u32 lane-ops/s
 HBM_PEAK_GBPS = 8000.0
-ROUND = "r03"
+ROUND = "r04"
 PROFILES = os.path.join(ROOT, "profiles", ROUND)
 LEGS = ["ecrecover", "chunk_root", "notary", "keccak", "tx_root", "poc", "headers", "pairing"]
 

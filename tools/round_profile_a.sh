@@ -3,7 +3,7 @@
 # all GPU tests, smoke, the default bench's kernel trace and the ecrecover / chunk_root / keccak
 # leg-only PMC passes (tools/profile_round.sh).  Part 2: tools/round_profile_b.sh.
 set -o pipefail
-R=${1:-r03}
+R=${1:-r04}
 O=gpurun_out/$R
 mkdir -p $O
 timeout -k 10 300 python -u tools/count_ops.py > $O/opcount.json 2> $O/opcount.err || { echo "opcount failed"; exit 1; }

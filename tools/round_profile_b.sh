@@ -3,7 +3,7 @@
 # default bench AFTER every PMC summary is in profiles/<round>/ of this tree (part 1's summaries were
 # copied there before this call), so bench.log reads the passes committed beside it.
 set -o pipefail
-R=${1:-r03}
+R=${1:-r04}
 O=gpurun_out/$R
 mkdir -p $O profiles/$R
 bash tools/profile_round.sh $R pairing notary || { echo "profile failed"; exit 1; }
