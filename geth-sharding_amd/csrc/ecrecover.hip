@@ -21,7 +21,10 @@
 //   * u1*G: fixed-base comb, 13 windows of 20 bits from a 1.09 GB affine table in HBM (one random
 //     80-byte entry per window, prefetched a window ahead), 13 mixed additions and no doublings
 //     (gsv_internal.h COMB_BITS; 16-bit windows from the Infinity Cache were 1.3 % slower).
-//   * one general Jacobian add to combine, one field inversion to affine, fused Keccak-256 address.
+//   * no square root up front: u2*R runs on the curve y^2 = x^3 + 7 c^3 (c = x^3 + 7) where R is
+//     (c x, c^2); one general add to combine, carried as a + t b (t = y_R); one exponentiation by
+//     (p-3)/4 then gives both y_R and Z^-1 (recover_dev.cuh GSV_RECOVER_TWIST); fused Keccak-256
+//     address.
 #include "opcount.cuh"
 #include "recover_dev.cuh"
 

@@ -310,6 +310,136 @@ GSV_DI void gej9_to_affine_words(fe& ax, fe& ay, const gej9& q) {
     fe9_to_words(ay.v, y);
 }
 
+// 1 (default): u2 R runs on the curve E_t: y^2 = x^3 + 7 c^3 (c = x_R^3 + 7), the image of E under
+// (x, y) -> (t^2 x, t^3 y) for t = y_R, where R is (c x_R, c^2) whatever t is, so no square root is
+// taken before the scalar multiplication.  A Jacobian (X, Y, Z) on E_t is (X, Y, t Z) on E; the sum with
+// u1 G is carried as a + t b, and ONE exponentiation at the end, w = (c z^4)^((p-3)/4) = 1/(s0 z^2)
+// with s0 = c^((p+1)/4), yields the root (s0 = c w z^2, t = +-s0 by the recid parity) and the inverse of
+// Z (1/(s0 z) = w z): the separate Z^-1 safegcd is gone.  0: the square root first, then the affine
+// conversion by safegcd (the round-3 form).
+#ifndef GSV_RECOVER_TWIST
+#define GSV_RECOVER_TWIST 1
+#endif
+
+// Q = P1 + P2 with P1 = u1 G on E (Jacobian, inf flag p1inf) and P2 = u2 R given on E_t as (X*, Y*, Z*)
+// (P2 on E = (X*, Y*, t Z*)), c = x_R^3 + 7, par = the parity y_R must have.  Returns false when c is
+// not a square (no R), u2 R = O or Q = O; otherwise (qx, qy) is Q in canonical words.
+// add-2001-b with Z2 = t Z*: Z2^2 = c Z*^2 is rational, S1 = Y1 Z2^3 = t S1' with S1' = Y1 Z* c Z*^2,
+// rr = S2 - t S1', and X3 = X3a + t X3b, Y3 = Y3a + t Y3b, Z3 = t z.  (tests/test_recover_twist.py
+// restates it with Python integers, exceptional cases included.)
+GSV_DI bool recover_tail_twisted(fe& qx, fe& qy, const gej9& p1, bool p1inf, const gej9& p2, bool p2inf,
+                                 const fe9& c, uint32_t par) {
+    fe9 x3a, db, y3a, y3b, z;  // X3b = -db
+    fe9 s1p, s2;
+    bool exc;
+    {
+        fe9 z1z1, zz, z2z2, u1, h, t;
+        fe9_sqr(z1z1, p1.z);                 // 2 -> 1
+        fe9_sqr(zz, p2.z);                   // 1
+        fe9_mul(z2z2, c, zz);                // Z2^2 = c Z*^2, 1
+        fe9_mul(u1, p1.x, z2z2);             // 1
+        fe9_neg<1>(t, u1);
+        fe9_mul_add(h, p2.x, z1z1, t);       // H = U2 - U1, 1 (weakly normalised)
+        fe9_mul(s1p, p1.y, p2.z);
+        fe9_mul(s1p, s1p, z2z2);             // S1', 1
+        fe9_mul(s2, p2.y, p1.z);             // 1*2
+        fe9_mul(s2, s2, z1z1);               // S2, 1
+        exc = !p1inf && fe9_is_zero_weak(h);
+        fe9 hh, hhh, v, cs1, a1;
+        fe9_sqr(hh, h);
+        fe9_mul(hhh, h, hh);                 // H^3
+        fe9_mul(v, u1, hh);                  // V = U1 H^2
+        fe9_mul(cs1, c, s1p);                // c S1'
+        fe9_negsum3<3>(t, hhh, v, v);        // -(H^3 + 2V)
+        fe9_sqr_add(a1, s2, t);              // S2^2 - H^3 - 2V, 1
+        fe9_mul_add(x3a, cs1, s1p, a1);      // X3a = S2^2 + c S1'^2 - H^3 - 2V, 1
+        fe9_mul(t, s2, s1p);
+        fe9_add(db, t, t);                   // db = 2 S2 S1' = -X3b, 2
+        fe9 da, ndb, e;
+        fe9_sub<1>(da, v, x3a);              // Da = V - X3a, 3
+        fe9_neg<2>(ndb, db);                 // 3
+        fe9_dot(y3a, s2, da, cs1, ndb);      // Y3a = S2 Da - c S1' Db, 1*3 + 1*3
+        fe9_add(e, da, hhh);                 // 4
+        fe9_normalize_weak(e);
+        fe9_neg<1>(t, e);                    // 2
+        fe9_dot(y3b, s2, db, s1p, t);        // Y3b = S2 Db - S1' (Da + H^3), 1*2 + 1*2
+        fe9_mul(t, p1.z, p2.z);              // 2*1
+        fe9_mul(z, t, h);                    // z = Z1 Z* H, 1
+    }
+    if (FE9_ANY(exc)) {  // P1 == +-P2 (rare; wave-uniform): 2 P2 on E_t, decided below by rr == 0
+        gej9 d;
+        gej9_dbl(d, p2);
+        fe9_cmov(x3a, d.x, exc);
+        fe9_cmov(y3a, d.y, exc);
+        fe9_cmov(z, d.z, exc);
+        fe9_cmov(db, s1p, exc);              // stash S1', S2 for the rr test
+        fe9_cmov(y3b, s2, exc);
+    }
+    if (FE9_ANY(p1inf)) {  // u1 G = O: Q = P2
+        fe9 zero;
+        fe9_set_u32(zero, 0);
+        fe9_cmov(x3a, p2.x, p1inf);
+        fe9_cmov(y3a, p2.y, p1inf);
+        fe9_cmov(z, p2.z, p1inf);
+        fe9_cmov(db, zero, p1inf);
+        fe9_cmov(y3b, zero, p1inf);
+    }
+    // the one exponentiation
+    fe9 m, s0;
+    bool ok;
+    {
+        fe9 z2, t, w;
+        fe9_sqr(z2, z);                      // z magnitude <= 2
+        fe9_sqr(t, z2);
+        fe9_mul(t, t, c);                    // c z^4
+        fe9_pow_pm3_4(w, t);                 // 1/(s0 z^2)
+        fe9_mul(m, w, z);                    // 1/(s0 z)
+        fe9_mul(t, c, m);
+        fe9_mul(s0, t, z);                   // s0 = c w z^2
+        fe9_sqr(t, s0);
+        fe9_normalize_full(t);
+        fe9 cc = c;
+        fe9_normalize_full(cc);
+        ok = fe9_eq_canon(t, cc) && !p2inf;  // c a square (R exists), u2 R != O
+    }
+    fe9 s0n = s0;
+    fe9_normalize_full(s0n);
+    bool flip = (s0n.v[0] & 1u) != par;     // t = -s0
+    fe9 pb, qb;
+    fe9_mul(pb, s0, db);                     // 1*2
+    fe9_mul(qb, s0, y3b);
+    if (FE9_ANY(exc)) {  // rr = S2 - t S1' = y3b - (+-pb): zero -> the doubling, else Q = O
+        fe9 a, b2;
+        fe9_add(a, y3b, pb);                 // t = -s0
+        fe9_sub<1>(b2, y3b, pb);             // t = s0
+        fe9_cmov(b2, a, flip);
+        bool rr0 = fe9_is_zero(b2);
+        ok = ok && !(exc && !rr0);
+        fe9 zero;
+        fe9_set_u32(zero, 0);
+        fe9_cmov(pb, zero, exc);
+        fe9_cmov(qb, zero, exc);
+    }
+    // x = (X3a - t db) m^2 with t = +-s0; y = Y3 / (t z)^3 = (+-Y3a + s0 Y3b) m^3 (1/t = +-1/s0)
+    fe9 m2, m3, n, xs, ys;
+    fe9_sqr(m2, m);
+    fe9_mul(m3, m2, m);
+    fe9_neg<1>(n, pb);
+    fe9_cmov(n, pb, flip);                   // -t db = -(+-s0) db
+    fe9_add(xs, x3a, n);                     // 1 + 2
+    fe9_neg<1>(n, y3a);
+    fe9_cmov(n, y3a, !flip);                 // sign(t) Y3a
+    fe9_add(ys, n, qb);                      // 2 + 1
+    fe9 x, y;
+    fe9_mul(x, xs, m2);
+    fe9_mul(y, ys, m3);
+    fe9_normalize_full(x);
+    fe9_normalize_full(y);
+    fe9_to_words(qx.v, x);
+    fe9_to_words(qy.v, y);
+    return ok;
+}
+
 // ---------------------------------------------------------------------------- recovery core
 // Returns GSV_ST_OK or GSV_ST_RECOVER_FAILED; on OK (qx, qy) is the affine public key.
 // msg/r/s are 256-bit values as little-endian limbs; recid in 0..3.
@@ -340,8 +470,18 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         }
         fe9_from_words(x, xw);
     }
-    // y = sqrt(x^3 + 7), parity recid & 1
     fe9 y, t;
+#if GSV_RECOVER_TWIST
+    // R on E_t (see recover_tail_twisted): (c x, c^2), c = x^3 + 7; the root is taken at the end
+    fe9 c;
+    fe9_sqr(t, x);
+    fe9_mul(c, t, x);
+    c.v[0] += 7u;
+    fe9_mul(t, c, x);
+    fe9_sqr(y, c);
+    x = t;
+#else
+    // y = sqrt(x^3 + 7), parity recid & 1
     fe9_sqr(t, x);
     fe9_mul(t, t, x);
     t.v[0] += 7u;
@@ -353,6 +493,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         fe9_normalize_weak(ny);
         fe9_cmov(y, ny, (y.v[0] & 1u) != (recid & 1u));
     }
+#endif
     // u1 = -m / r, u2 = s / r
     sc rn, u1, u2;
     modinv30_words(rn.v, rs.v, MI30_N);  // r^-1 mod n (safegcd; r != 0 on every valid path)
@@ -603,7 +744,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             ainf = tinf;
         }
     }
-    fe9_mul(acc.z, acc.z, zfac);  // back from E'' to E (2*1 -> 1)
+    fe9_mul(acc.z, acc.z, zfac);  // back from E'' to E (E_t with GSV_RECOVER_TWIST; 2*1 -> 1)
 
     // ---- u1 * G via comb
     gej9 accg;
@@ -611,11 +752,15 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     comb_mul_g9(accg, ginf, u1, gtab);
 
     // ---- Q = u2 R + u1 G
+#if GSV_RECOVER_TWIST
+    ok = recover_tail_twisted(qx, qy, accg, ginf, acc, ainf, c, recid & 1u) && ok;
+#else
     gej9 q;
     bool qinf;
     gej9_add(q, qinf, acc, ainf, accg, ginf);
     ok = ok && !qinf;
     gej9_to_affine_words(qx, qy, q);
+#endif
     return ok ? GSV_ST_OK : GSV_ST_RECOVER_FAILED;
 }
 
