@@ -145,8 +145,9 @@ def fe9_case(rng, ma, mb, extreme):
 
 
 OPND1 = {"r": 0, "a": 18, "b": 27, "k31264": 36, "k256": 37, "k977": 38, "c": 39, "d": 48}
-# the two column forms of tools/gen_fe9_asm.py (GSV_FE9_COLS 1 / 2) and their operand numbering
-FORMS = {1: (gen_fe9_asm.full_lines, OPND1), 2: (gen_fe9_asm.full_lines2, gen_fe9_asm.OPND2)}
+# the column forms of tools/gen_fe9_asm.py (GSV_FE9_COLS 1 / 2 / 3) and their operand numbering
+FORMS = {1: (gen_fe9_asm.full_lines, OPND1), 2: (gen_fe9_asm.full_lines2, gen_fe9_asm.OPND2),
+         3: (gen_fe9_asm.full_lines3, gen_fe9_asm.OPND2)}
 
 
 def fe9_lines(form, terms, addend=False):
@@ -176,7 +177,7 @@ def check_weak(r, want):
 
 
 @pytest.mark.parametrize("ma,mb", [(1, 1), (1, 7), (7, 1), (2.64, 2.64), (2, 3.5)])
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("form", [1, 2, 3])
 def test_fe9_mul_asm(form, ma, mb):
     rng = random.Random(int(ma * 100 + mb))
     lines = fe9_lines(form, gen_fe9_asm.MUL_TERMS)
@@ -186,7 +187,7 @@ def test_fe9_mul_asm(form, ma, mb):
 
 
 @pytest.mark.parametrize("ma", [1, 2, 2.64])
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("form", [1, 2, 3])
 def test_fe9_sqr_asm(form, ma):
     rng = random.Random(int(ma * 100))
     lines = fe9_lines(form, gen_fe9_asm.SQR_TERMS)
@@ -208,7 +209,7 @@ def addend_case(rng, extreme):
 
 
 @pytest.mark.parametrize("ma,mb", [(1.04, 1.04), (1, 3), (1.04, 4.16), (1, 7)])
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("form", [1, 2, 3])
 def test_fe9_mul_add_asm(form, ma, mb):
     rng = random.Random(int(ma * 1000 + mb))
     lines = fe9_lines(form, gen_fe9_asm.MUL_TERMS, addend=True)
@@ -219,7 +220,7 @@ def test_fe9_mul_add_asm(form, ma, mb):
 
 
 @pytest.mark.parametrize("ma", [1, 1.04, 2.64])
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("form", [1, 2, 3])
 def test_fe9_sqr_add_asm(form, ma):
     rng = random.Random(int(ma * 1000) + 7)
     lines = fe9_lines(form, gen_fe9_asm.SQR_TERMS, addend=True)
@@ -231,7 +232,7 @@ def test_fe9_sqr_add_asm(form, ma):
 
 
 @pytest.mark.parametrize("m", [(1.04, 3.04, 1.04, 3), (1, 3.5, 1, 3.5), (1.04, 1.04, 2.64, 2.2)])
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("form", [1, 2, 3])
 def test_fe9_dot_asm(form, m):
     """a*b + c*d with one reduction at m_a m_b + m_c m_d <= 7 (the mixed add's Y3: rr (V - X3) + Y1 (-2J))"""
     ma, mb, mc, md = m
@@ -250,7 +251,7 @@ def _q_consts():
     return {m + 1: [int(x.strip().rstrip("u"), 16) for x in rows[m].strip().strip("{},").split(",")] for m in range(7)}
 
 
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("form", [1, 2, 3])
 def test_fe9_dot_asm_at_the_mixed_add_operands(form):
     """the operands fe9_dot actually gets in gej9_add_ge_core, at their largest limbs: rr and Y1 are
     product outputs (limb 2 up to 2^29 + 2^24), V - X3 = V + (Q_1 - X3), -2J = Q_2 - J - J (limb 8

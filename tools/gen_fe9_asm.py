@@ -217,8 +217,77 @@ def full_lines2(terms_of_column, addend=False):
     return L
 
 
-def full2(name, doc, terms_of_column, addend=False, dot=False):
-    L = full_lines2(terms_of_column, addend)
+# ---------------------------------------------------------------------------- column form 3
+def full_lines3(terms_of_column, addend=False):
+    """Form 3: form 2's high columns, computed FIRST (column 9 from 0 instead of column 8's carry),
+    and the low columns 0..8 never carried on their own: limb j's running value is the reduction's
+    carry + column j's products + 31264 o_{j+9} + 256 o_{j+8} (+ c_j), one 64-bit multiply-add chain,
+    then one mask and one 64-bit shift.  Form 2 carried every low column (shift + mask) and then ran
+    the reduction's own carry chain over the masked limbs (a 32-bit add, a mask and a shift again):
+    per product 9 64-bit shifts, 9 masks and 9 adds fewer.  Bounds: a column's products sum to
+    < 63 2^58 (the m_a m_b <= 7 precondition), the carry is < 2^35, the folds < 2^47 + 2^40 and the
+    addend < 2^31: < 2^64.  Limb 8's remainder c >> 24 < 2^40 and o17 < 2^32 make T < 2^46.  With an
+    addend, c_j enters as one multiply-add by 1 (the three-operand add of form 2 is gone with the
+    separate column carry)."""
+    O = OPND2
+    opnd = lambda x: f"%{O['a'] + x}" if x < 9 else (f"%{O['b'] + x - 9}" if x < 18 else f"%{O['c'] + x - 18}")
+    cj = lambda j: f"%{O['c'] + j}"
+    r = lambda k: f"%{O['r'] + k}"
+    C, c0, c1 = "v[2:3]", "v2", "v3"
+    D, d0, d1 = "v[4:5]", "v4", "v5"
+    lo = lambda k: "v2" if k == 9 else f"v{6 + 2 * (k - 10)}"
+    hi = lambda k: "v3" if k == 9 else f"v{7 + 2 * (k - 10)}"
+    K31264, K256, K977, SD = f"%{O['k31264']}", f"%{O['k256']}", f"%{O['k977']}", f"%{O['sd']}"
+    K8192 = f"%{O['k8192']}"
+    L = []
+    for k in range(9, 17):                                 # high columns: form 2's chains
+        if k == 9:
+            acc, first = C, True
+        else:
+            acc = PAIR2[k]
+            L.append(f"v_mad_u64_u32 {acc}, {SD}, {hi(k - 1)}, 8, 0")
+            first = False
+        for (x, y) in terms_of_column(k):
+            L.append(f"v_mad_u64_u32 {acc}, {SD}, {opnd(x)}, {opnd(y)}, {'0' if first else acc}")
+            first = False
+    L.append(f"v_lshlrev_b32 {c1}, 3, {hi(16)}")           # o17 = 8 hi(P_16) < 2^32
+    for j in range(9):                                     # low limbs: products + folds, one carry
+        first = j == 0
+        if addend:
+            L.append(f"v_mad_u64_u32 {D}, {SD}, {cj(j)}, 1, {'0' if first else D}")
+            first = False
+        for (x, y) in terms_of_column(j):
+            L.append(f"v_mad_u64_u32 {D}, {SD}, {opnd(x)}, {opnd(y)}, {'0' if first else D}")
+            first = False
+        if j < 8:
+            L.append(f"v_mad_u64_u32 {D}, {SD}, {lo(j + 9)}, {K31264}, {D}")
+            if j:
+                L.append(f"v_mad_u64_u32 {D}, {SD}, {lo(j + 8)}, {K256}, {D}")
+            L.append(f"v_and_b32_e32 {r(j)}, 0x1fffffff, {d0}")
+            L.append(f"v_lshrrev_b64 {D}, 29, {D}")       # carry < 2^35
+        else:
+            L.append(f"v_mad_u64_u32 {D}, {SD}, {c1}, {K31264}, {D}")
+            L.append(f"v_mad_u64_u32 {D}, {SD}, {lo(16)}, {K256}, {D}")
+            L.append(f"v_and_b32_e32 {r(8)}, 0xffffff, {d0}")
+            L.append(f"v_lshrrev_b64 {D}, 24, {D}")
+    T, t0, t1 = "v[6:7]", "v6", "v7"                      # P_10 is dead by now
+    L.append(f"v_mad_u64_u32 {T}, {SD}, {c1}, {K8192}, {D}")  # T = (c >> 24) + o17 2^13 < 2^46
+    L.append(f"v_mov_b32 {d1}, 0")
+    L.append(f"v_mov_b32 {d0}, {r(0)}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {t0}, {K977}, {D}")
+    L.append(f"v_mad_u32_u24 {d1}, {t1}, {K977}, {d1}")
+    L.append(f"v_and_b32_e32 {r(0)}, 0x1fffffff, {d0}")
+    L.append(f"v_lshrrev_b64 {D}, 29, {D}")
+    L.append(f"v_lshl_add_u64 {D}, {T}, 3, {D}")
+    L.append(f"v_mad_u64_u32 {D}, {SD}, {r(1)}, 1, {D}")
+    L.append(f"v_and_b32_e32 {r(1)}, 0x1fffffff, {d0}")
+    L.append(f"v_alignbit_b32 {t0}, {d1}, {d0}, 29")
+    L.append(f"v_add_u32 {r(2)}, {r(2)}, {t0}")
+    return L
+
+
+def full2(name, doc, terms_of_column, addend=False, dot=False, gen=None):
+    L = (gen or full_lines2)(terms_of_column, addend)
     outs = ", ".join([f'"=&v"(r[{i}])' for i in range(9)] + ['"=&s"(sd)'])
     ins = ", ".join([f'"v"(a[{i}])' for i in range(9)] + [f'"v"(b[{j}])' for j in range(9)] +
                     ['"s"(k31264)', '"s"(k256)', '"s"(k977)', '"s"(k8192)'] +
@@ -240,9 +309,10 @@ def full2(name, doc, terms_of_column, addend=False, dot=False):
 def main():
     out = ["// GENERATED by tools/gen_fe9_asm.py — do not edit by hand.",
            "// Column products of secp256k1_fe9.cuh as single inline-asm statements (see the generator's",
-           "// docstring for why).  GSV_FE9_COLS selects the column form: 2 (default) keeps the high columns",
-           "// 9..16 unmasked in fixed register pairs (full_lines2), 1 masks and shifts every column.",
-           "#pragma once", "#include <stdint.h>", "#ifndef GSV_FE9_COLS", "#define GSV_FE9_COLS 2", "#endif",
+           "// docstring for why).  GSV_FE9_COLS selects the column form: 3 (default) runs the low columns inside",
+           "// the reduction's carry chain (full_lines3), 2 keeps the high columns 9..16 unmasked in fixed",
+           "// register pairs (full_lines2), 1 masks and shifts every column.",
+           "#pragma once", "#include <stdint.h>", "#ifndef GSV_FE9_COLS", "#define GSV_FE9_COLS 3", "#endif",
            "namespace gsv {"]
     specs = [("fe9_mul_full", "r = a * b mod p, weakly normalised (fe9_mul's contract)", MUL_TERMS, False, False),
              ("fe9_sqr_full", "r = a^2 mod p with b = 2a limb-wise (fe9_sqr's contract)", SQR_TERMS, False, False),
@@ -253,9 +323,12 @@ def main():
     out.append("#if GSV_FE9_COLS == 1")
     for name, doc, terms, add, dot in specs:
         out += full(name, doc, terms, add, dot)
-    out.append("#else")
+    out.append("#elif GSV_FE9_COLS == 2")
     for name, doc, terms, add, dot in specs:
         out += full2(name, doc, terms, add, dot)
+    out.append("#else")
+    for name, doc, terms, add, dot in specs:
+        out += full2(name, doc, terms, add, dot, gen=full_lines3)
     out.append("#endif")
     out.append("}  // namespace gsv")
     with open(OUT, "w") as f:
