@@ -385,8 +385,8 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
             "algorithmic_per_unit": "256-bit products as 8x8 32x32-bit partial products (mul 64, sqr 36): "
                                     f"{MACS_PER_RECOVERY_REF} per recovery for the reference algorithm "
                                     "(libsecp256k1 Strauss-wNAF), mac_equiv_per_recovery_actual = the "
-                                    "v_mad_u64_u32 our kernel executes per recovery (9x29-bit fe9 products 100, "
-                                    "squarings 64; GLV w=4 + comb; instrumented build, profiles/{ROUND}/opcount.json)".format(ROUND=ROUND)}
+                                    "v_mad_u64_u32 our kernel executes per recovery (9x29-bit fe9 products 108, "
+                                    "squarings 72, dot products 189; GLV w=4 + comb; instrumented build, profiles/{ROUND}/opcount.json)".format(ROUND=ROUND)}
     state = {"msg": msg, "sig": sig, "epub": epub}
     return {"rate": rate, "dt": dt, "roofline": roof}, state
 

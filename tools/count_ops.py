@@ -8,7 +8,9 @@ tools/build_variant.sh opcount -DGSV_OPCOUNT`), at the bench's batch sizes:
 
 "mad" is the number of v_mad_u64_u32 (32 x 32 -> 64-bit multiply-adds: the unit of the VALU MAC
 roofline) our kernels execute, from the op counts and each op's mad count in our limb layout:
-a secp256k1 fe9 product 81 + 19 (the 2^261 fold, secp256k1_fe9.cuh fe9_reduce), a squaring 45 + 19,
+a secp256k1 fe9 product 81 + 27 (column form 3 of tools/gen_fe9_asm.py: 7 high-column carries, 17
+2^261 folds, 3 in the 2^256 fold; a product with an addend has 9 more, counted as a product), a
+squaring 45 + 27, a dot product 162 + 27,
 a scalar product 64 (8 x 32-bit limbs; the folds mod n are not counted, < 1 %), a BN254 F_p product
 81 (9 x 29-bit) and a BN254 Montgomery reduction 81 (one per fq_mul / fq_mul2 / fq_dot, shared by
 the products it sums).  Safegcd inversions are counted separately (their divsteps are not mads).
@@ -48,7 +50,7 @@ def per_unit(c, n):
 def main():
     ctx = gsv.Context(0)
     dev = torch.device("cuda", 0)
-    W = {"fe_mul": 100, "fe_sqr": 64, "sc_mul": 64, "sc_sqr": 36, "bn_mul": 81, "bn_redc": 81, "fe_dot": 181}
+    W = {"fe_mul": 108, "fe_sqr": 72, "sc_mul": 64, "sc_sqr": 36, "bn_mul": 81, "bn_redc": 81, "fe_dot": 189}
     out = {"build": "variants/opcount (-DGSV_OPCOUNT)", "unit": "v_mad_u64_u32 per unit of work",
            "weights_mad_per_op": W}
     # ---- configs[1]: 2^20 recoveries
