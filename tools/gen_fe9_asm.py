@@ -218,6 +218,10 @@ def full_lines2(terms_of_column, addend=False):
 
 
 # ---------------------------------------------------------------------------- column form 3
+# 1: the high columns emitted round-robin across their independent chains (measured equal at two
+# waves per SIMD, profiles/r04/ab/il_*.json: the other wave already hides the chains' latency)
+INTERLEAVE3 = os.environ.get("GSV_FE9_INTERLEAVE", "0") == "1"
+
 def full_lines3(terms_of_column, addend=False):
     """Form 3: form 2's high columns, computed FIRST (column 9 from 0 instead of column 8's carry),
     and the low columns 0..8 never carried on their own: limb j's running value is the reduction's
@@ -240,16 +244,31 @@ def full_lines3(terms_of_column, addend=False):
     K31264, K256, K977, SD = f"%{O['k31264']}", f"%{O['k256']}", f"%{O['k977']}", f"%{O['sd']}"
     K8192 = f"%{O['k8192']}"
     L = []
-    for k in range(9, 17):                                 # high columns: form 2's chains
-        if k == 9:
-            acc, first = C, True
-        else:
-            acc = PAIR2[k]
-            L.append(f"v_mad_u64_u32 {acc}, {SD}, {hi(k - 1)}, 8, 0")
-            first = False
-        for (x, y) in terms_of_column(k):
-            L.append(f"v_mad_u64_u32 {acc}, {SD}, {opnd(x)}, {opnd(y)}, {'0' if first else acc}")
-            first = False
+    acc_of = lambda k: C if k == 9 else PAIR2[k]
+    if INTERLEAVE3:
+        # the eight high columns' product chains are independent: emitted round-robin (one term of
+        # each column in turn), each from 0; the carries 8 hi(P_{k-1}) follow as one short chain
+        cols = {k: list(terms_of_column(k)) for k in range(9, 17)}
+        for t in range(max(len(v) for v in cols.values())):
+            for k in range(9, 17):
+                if t < len(cols[k]):
+                    x, y = cols[k][t]
+                    acc = acc_of(k)
+                    L.append(f"v_mad_u64_u32 {acc}, {SD}, {opnd(x)}, {opnd(y)}, {'0' if t == 0 else acc}")
+        for k in range(10, 17):
+            acc = acc_of(k)
+            L.append(f"v_mad_u64_u32 {acc}, {SD}, {hi(k - 1)}, 8, {acc if cols[k] else '0'}")
+    else:
+        for k in range(9, 17):                             # high columns: form 2's chains
+            if k == 9:
+                acc, first = C, True
+            else:
+                acc = PAIR2[k]
+                L.append(f"v_mad_u64_u32 {acc}, {SD}, {hi(k - 1)}, 8, 0")
+                first = False
+            for (x, y) in terms_of_column(k):
+                L.append(f"v_mad_u64_u32 {acc}, {SD}, {opnd(x)}, {opnd(y)}, {'0' if first else acc}")
+                first = False
     L.append(f"v_lshlrev_b32 {c1}, 3, {hi(16)}")           # o17 = 8 hi(P_16) < 2^32
     for j in range(9):                                     # low limbs: products + folds, one carry
         first = j == 0
