@@ -141,6 +141,27 @@ def ecrecover_fixtures():
         r = rng.randrange(1, pmn)
         add(bytes(rng.getrandbits(8) for _ in range(32)), _sig(r, rng.randrange(1, N_ORDER), 2 + (t & 1)),
             "r < p-n, recid>=2")
+    # the exceptional cases of the final u1 G + u2 R sum (recover_dev.cuh recover_tail_twisted decides
+    # them after the root's sign is known): R = k G, m = -s k mod n gives u1 G == u2 R (the sum is a
+    # doubling, Q = 2 u2 R, recovers); the opposite recid parity turns R into -R, which swaps the two
+    # constructions (m = s k then doubles, m = -s k reaches infinity)
+    rng2 = random.Random(3)
+    for t in range(6):
+        while True:
+            k = rng2.randrange(1, N_ORDER)
+            pub = ctypes.create_string_buffer(65)
+            R.gsvref_pubkey(pub, k.to_bytes(32, "big"))
+            x = int.from_bytes(pub.raw[1:33], "big")
+            y = int.from_bytes(pub.raw[33:65], "big")
+            if x < N_ORDER:
+                break
+        s = rng2.randrange(1, N_ORDER)
+        for flip in (0, 1):
+            for sign in (1, -1):
+                m = sign * s * k % N_ORDER
+                want = "doubling (recovers)" if (sign == -1) != bool(flip) else "infinity (fails)"
+                add(m.to_bytes(32, "big"), _sig(x, s, (y & 1) ^ flip),
+                    f"u1 G == {'-' if 'inf' in want else '+'}u2 R: {want}")
     dump("ecrecover.json", {"cases": cases})
 
 
