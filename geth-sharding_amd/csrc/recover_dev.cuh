@@ -40,7 +40,7 @@ __device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du
 #endif
 constexpr int GLV_W = GSV_GLV_W;
 constexpr int GLV_NT = 1 << (GLV_W - 1);             // table entries
-constexpr int GLV_DIGITS = (130 + GLV_W - 1) / GLV_W;  // k + skew < 2^129 (the split's bound is 2^128)
+constexpr int GLV_DIGITS = (130 + GLV_W - 1) / GLV_W;  // |k| < 2^130: the split gives < 2^128, + skew or a lattice vector (GSV_GLV_ODD) < 2^129.3
 // digit code = sign bit above a (W - 1)-bit table index, packed in DIG_SLOT-bit slots
 constexpr int DIG_SLOT = GLV_W <= 4 ? 4 : 8;
 constexpr int DIG_PER_WORD = 32 / DIG_SLOT;
@@ -440,6 +440,37 @@ GSV_DI bool recover_tail_twisted(fe& qx, fe& qy, const gej9& p1, bool p1inf, con
     return ok;
 }
 
+// 1 (default): both GLV halves are made odd before the recoding by adding a vector of the GLV lattice
+// ({(a, b) : a + b lambda == 0 mod n}, libsecp256k1 scalar_impl.h's basis), so the odd-digit recoding
+// needs no skew and the two skew-correcting mixed adds at the end of u2 R disappear.  v1 = (a1, b1)
+// has odd/odd coordinates, v2 = (a2, a1) even/odd, v1 + v2 odd/even: one of them (or none) turns the
+// magnitudes |k1|, |k2| (parity of k mod n XOR its sign, n being odd) both odd.  |a1| < 2^126,
+// |b1| < 2^128, |a2| < 2^129: |k| < 2^128 grows below 2^129.3 < 2^130, inside GLV_DIGITS' range.
+#ifndef GSV_GLV_ODD
+#define GSV_GLV_ODD 1
+#endif
+__device__ constexpr uint32_t GLV_V1A[8] = {0x9284EB15u, 0xE86C90E4u, 0xA7D46BCDu, 0x3086D221u, 0u, 0u, 0u, 0u};
+__device__ constexpr uint32_t GLV_V1B[8] = {0xC5765C7Eu, 0x507DDEE3u, 0xAE3A1813u, 0xD66B5E10u,
+                                            0xFFFFFFFDu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+__device__ constexpr uint32_t GLV_V2A[8] = {0x9D44CFD8u, 0x57C1108Du, 0xA8E2F3F6u, 0x14CA50F7u, 1u, 0u, 0u, 0u};
+__device__ constexpr uint32_t GLV_V3A[8] = {0x2FC9BAEDu, 0x402DA172u, 0x50B75FC4u, 0x45512319u, 1u, 0u, 0u, 0u};
+__device__ constexpr uint32_t GLV_V3B[8] = {0x57FB4793u, 0x38EA6FC8u, 0x560E83E1u, 0x06F23032u,
+                                            0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+GSV_DI void glv_make_odd(sc& k1, sc& k2) {
+    bool odd1 = ((k1.v[0] & 1u) != 0) != sc_is_high(k1);  // parity of |k1|
+    bool odd2 = ((k2.v[0] & 1u) != 0) != sc_is_high(k2);
+    // (flip k1, flip k2): (1, 1) v1, (0, 1) v2 = (a2, a1), (1, 0) v1 + v2, (0, 0) nothing
+    bool use1 = !odd1 && !odd2, use2 = odd1 && !odd2, use3 = !odd1 && odd2;
+    sc A, B;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        A.v[i] = use1 ? GLV_V1A[i] : use2 ? GLV_V2A[i] : use3 ? GLV_V3A[i] : 0u;
+        B.v[i] = use1 ? GLV_V1B[i] : use2 ? GLV_V1A[i] : use3 ? GLV_V3B[i] : 0u;
+    }
+    sc_add(k1, k1, A);
+    sc_add(k2, k2, B);
+}
+
 // ---------------------------------------------------------------------------- recovery core
 // Returns GSV_ST_OK or GSV_ST_RECOVER_FAILED; on OK (qx, qy) is the affine public key.
 // msg/r/s are 256-bit values as little-endian limbs; recid in 0..3.
@@ -504,6 +535,9 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     // ---- u2 * R via GLV + fixed w = GLV_W odd digits
     sc k1, k2;
     sc_split_lambda(k1, k2, u2);
+#if GSV_GLV_ODD
+    glv_make_odd(k1, k2);
+#endif
     bool neg1 = sc_is_high(k1), neg2 = sc_is_high(k2);
     {
         sc nk;
@@ -713,8 +747,9 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     }
 #endif
     // skew corrections: the recoded scalars were k + skew -> subtract (+-)T0 / (+-)lambda(T0)
+    // (GSV_GLV_ODD: both halves are odd, the skews are 0 and there is nothing to correct)
 #pragma unroll 1
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < (GSV_GLV_ODD ? 0 : 2); j++) {
         bool ng = j ? neg2 : neg1;
         uint32_t sk = j ? skew2 : skew1;
         ge9 P;
