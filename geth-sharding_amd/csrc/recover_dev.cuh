@@ -268,11 +268,16 @@ GSV_DI uint32_t comb_digit(const sc& u, uint32_t w) {
 
 // u*G with the fixed-base comb table (COMB_WINDOWS mixed adds, no doublings)
 GSV_DI void comb_mul_g9(gej9& acc, bool& inf, const sc& u, const uint4* __restrict__ gtab) {
-    inf = true;
     ge9 Pn;
     gtab_load(Pn, gtab + (size_t)comb_digit(u, 0) * GTAB_ENTRY_U4);
+    // window 0 starts the sum: its entry is the accumulator (Z = 1), no add
+    acc.x = Pn.x;
+    acc.y = Pn.y;
+    fe9_set_u32(acc.z, 1);
+    inf = comb_digit(u, 0) == 0;
+    gtab_load(Pn, gtab + (((size_t)1 << COMB_BITS) + comb_digit(u, 1)) * GTAB_ENTRY_U4);
 #pragma unroll 1
-    for (int w = 0; w < COMB_WINDOWS; w++) {
+    for (int w = 1; w < COMB_WINDOWS; w++) {
         uint32_t d = comb_digit(u, (uint32_t)w);
         ge9 P = Pn;
         if (w < COMB_WINDOWS - 1) {  // prefetch next window's entry
@@ -742,6 +747,14 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             fe9 ny;
             fe9_neg<1>(ny, P.y);         // 2
             fe9_cmov(P.y, ny, ((c >> (GLV_W - 1)) != 0) != ng);
+            if (i == GLV_DIGITS - 1 && j == 0) {  // the top digit starts the sum (Z = 1), no add
+                acc.x = P.x;
+                acc.y = P.y;
+                fe9_normalize_weak(acc.y);
+                fe9_set_u32(acc.z, 1);
+                ainf = false;
+                continue;
+            }
             gej9_add_ge(acc, ainf, acc, P);
         }
     }
