@@ -407,6 +407,7 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
     roots = rootk[0]
     ctx.chunk_root_prepare(h_off)
     ctx.set_pipeline_depth(1)
+    torch.cuda.synchronize()  # the inputs were staged on torch's default stream
     csteps = max(4, args.steps)
     for i in range(max(depth, args.warmup)):
         ctx.chunk_root_batch_dev(bodies, h_off, rootk[i % depth], stream=streams[i % depth], prepare=False)
@@ -620,6 +621,7 @@ def leg_keccak(ctx, stream, dev, ws, rank, args):
     vals = torch.from_numpy(vals_np).to(dev)
     koff_t = torch.from_numpy(voff.astype(np.int64)).to(dev)
     kout = torch.empty((nblk * ntx, 32), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # the inputs were staged on torch's default stream
     ctx.keccak256_batch_dev(vals, koff_t, kout, stream=stream)
     stream.synchronize()
     ksteps = 5
@@ -677,6 +679,7 @@ def leg_tx_root(ctx, stream, dev, ws, rank, args):
     list_off = np.arange(nblk + 1, dtype=np.uint64) * ntx
     troots = torch.empty((nblk, 32), dtype=torch.uint8, device=dev)
     ctx.derive_sha_prepare(voff, list_off)
+    torch.cuda.synchronize()  # the inputs were staged on torch's default stream
     ctx.derive_sha_batch_dev(vals, voff, list_off, troots, stream=stream, prepare=False)
     stream.synchronize()
     tsteps = 3
@@ -706,6 +709,7 @@ def leg_poc(ctx, stream, dev, ws, rank, args):
     salt = bytes(range(1, 21))
     pocs = torch.empty((N_SHARDS, 32), dtype=torch.uint8, device=dev)
     ctx.collation_poc_prepare(p_off, salt)
+    torch.cuda.synchronize()  # the inputs were staged on torch's default stream
     ctx.collation_poc_batch_dev(pbodies, p_off, salt, pocs, stream=stream, prepare=False)
     stream.synchronize()
     qsteps = 2
@@ -734,6 +738,7 @@ def leg_headers(ctx, stream, dev, ws, rank, args, sig):
     hprop = torch.randint(0, 256, (nh, 20), dtype=torch.uint8, device=dev)
     hst = torch.empty((nh,), dtype=torch.uint8, device=dev)
     hhash = torch.empty((nh, 32), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # the inputs were staged on torch's default stream
     ctx.collation_header_verify_batch_dev(hsid, hroot, hper, hprop, sig, hst, None, hhash, None, stream=stream)
     stream.synchronize()
     assert bool((hst == _lib.ST_PROPOSER_MISMATCH).all()), "header signatures failed to recover"
@@ -756,6 +761,7 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     pin = torch.empty((nloc, 768), dtype=torch.uint8, device=dev)
     pexp = torch.empty((nloc,), dtype=torch.uint8, device=dev)
     pver = torch.empty((nloc,), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # the inputs were staged on torch's default stream
     ctx.bn256_synth_checks_dev(5000 + rank, pin, pexp, stream=stream)
     p_off = np.arange(nloc + 1, dtype=np.uint64) * 768
     stream.synchronize()

@@ -528,7 +528,10 @@ int gsv_ctx_create(int device, gsv_ctx** out) {
     HIPCHK(hipSetDevice(device));
     gsv_ctx* c = new gsv_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    // a BLOCKING stream: a *_dev call made with stream = NULL is ordered with the legacy default
+    // (NULL) stream of the process both ways — a caller's prior fills and copies there (e.g. PyTorch's
+    // default stream) complete before it, and later default-stream work sees its results
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {
         delete c;
         return GSV_E_HIP;
     }

@@ -47,6 +47,9 @@
  *     uses of the same shape (non-captured calls on different streams are ordered by the library).
  *   - One gsv_ctx per device; a context is safe to use from several threads on distinct streams
  *     for the *_dev calls; host-pointer calls serialize on the context's internal stream.
+ *   - stream = NULL selects the context stream, a blocking stream: it is ordered both ways with work
+ *     on the process's legacy default (NULL) stream, such as PyTorch's default stream.  Work on other
+ *     non-blocking streams is the caller's to order (events), as for any stream argument.
  */
 #ifndef GSV_H
 #define GSV_H

@@ -230,6 +230,7 @@ def test_dev_calls_capture_into_a_hip_graph(ctx, oracle):
         t.zero_()
     st.fill_(9)
     es = torch.cuda.Stream()
+    es.wait_stream(torch.cuda.current_stream())  # the zero / fill above run on the default stream
     enqueue(es)
     es.synchronize()
     eager = (pub, addr, st, kout, roots, pocs, pver, troots, hst, hhash)
@@ -285,6 +286,8 @@ def test_pipeline_depth_instances_run_concurrently_and_agree(ctx, oracle):
     ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
     roots = [torch.zeros((len(lens), 32), dtype=torch.uint8, device=dev) for _ in range(4)]
     pv = [torch.full((nchk,), 7, dtype=torch.uint8, device=dev) for _ in range(4)]
+    for s in ss:
+        s.wait_stream(torch.cuda.current_stream())  # the zero / fill above run on the default stream
     for i in range(4):  # calls 0, 2 on stream 0 and 1, 3 on stream 1: the two instances in flight together
         ctx.chunk_root_batch_dev(bodies, h_off, roots[i], stream=ss[i % 2], prepare=False)
         ctx.pairing_check_batch_dev(pin, p_off, pv[i], stream=ss[i % 2], prepare=False)

@@ -174,6 +174,7 @@ def test_dev_calls_on_two_streams_share_the_workspace_safely(ctx, oracle):
         dev = torch.tensor(np.frombuffer(b"".join(bodies), np.uint8).copy(), device="cuda")
         roots = torch.zeros((len(bodies), 32), dtype=torch.uint8, device="cuda")
         st = s1 if k % 2 == 0 else s2
+        st.wait_stream(torch.cuda.current_stream())  # the copy and zero fill run on the default stream
         ctx.chunk_root_batch_dev(dev, off, roots, stream=st)
         jobs.append((bodies, roots, dev))
     salt = bytes(range(3, 23))
@@ -182,6 +183,7 @@ def test_dev_calls_on_two_streams_share_the_workspace_safely(ctx, oracle):
     poff[1:] = np.cumsum([len(b) for b in pb])
     pdev = torch.tensor(np.frombuffer(b"".join(pb) + b"\0", np.uint8).copy(), device="cuda")
     pocs = torch.zeros((3, 32), dtype=torch.uint8, device="cuda")
+    s2.wait_stream(torch.cuda.current_stream())
     ctx.collation_poc_batch_dev(pdev, poff, salt, pocs, stream=s2)
     torch.cuda.synchronize()
     for bodies, roots, _ in jobs:

@@ -164,8 +164,10 @@ def _rank_worker(rank, world, port, nsh, txs, q):
         ctx.notary_partition_unpack_dev(allb_t, nsh, world, g_root, g_ntx, g_bm, g_rst, max_txs=txs)
         torch.cuda.synchronize()
         g_root, g_ntx, g_bm = g_root.cpu(), g_ntx.cpu(), g_bm.cpu()
-        assert (g_rst.cpu() == 0).all()
-        assert torch.equal(g_root, t_root) and torch.equal(g_ntx, t_ntx) and torch.equal(g_bm, t_bm)
+        assert (g_rst.cpu() == 0).all(), f"rank statuses {g_rst.cpu().tolist()}"
+        for nm, a, b in (("root", g_root, t_root), ("ntx", g_ntx, t_ntx), ("bitmap", g_bm, t_bm)):
+            bad = [i for i in range(nsh) if not torch.equal(a[i], b[i])]
+            assert not bad, f"C-ABI vs torch gather: {nm} differs at shards {bad[:8]} (this rank: {lo}..{hi - 1})"
         # the whole batch validated in this process
         allb = torch.empty((nsh * txs * 128,), dtype=torch.uint8, device=dev)
         ctx.notary_synth_dev(4242, 0, nsh, txs, allb)
@@ -173,8 +175,12 @@ def _rank_worker(rank, world, port, nsh, txs, q):
         flat = allb.cpu().numpy()
         want = ctx.notary_validate_shards([flat[i * txs * 128:(i + 1) * txs * 128].tobytes() for i in range(nsh)],
                                           max_txs=txs)
-        ok = (np.array_equal(g_root.numpy(), want[0]) and np.array_equal(g_ntx.numpy(), want[1])
-              and np.array_equal(g_bm.numpy(), want[2]))
+        ok = True
+        for nm, a, b in (("root", g_root.numpy(), want[0]), ("ntx", g_ntx.numpy(), want[1]), ("bitmap", g_bm.numpy(), want[2])):
+            bad = [i for i in range(nsh) if not np.array_equal(a[i], b[i])]
+            if bad:
+                ok = f"gathered vs whole batch: {nm} differs at shards {bad[:8]} (this rank: {lo}..{hi - 1})"
+                break
         q.put((rank, ok))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
