@@ -618,10 +618,12 @@ enum : uint8_t { CS_OK = 0, CS_BAD = 1, CS_ONE = 2 };  // CS_ONE: no finite pair
 #ifndef BN_MILLER_WAVES
 #define BN_MILLER_WAVES 1
 #endif
-// 1: k_bn_miller loads each line one multiplication ahead (Miller 9.0 -> 8.8 ms at 65,536 checks,
-// profiles/r02/ab_miller_prefetch.txt)
+// 1: k_bn_miller loads each line one multiplication ahead (r02: Miller 9.0 -> 8.8 ms at 65,536
+// checks, profiles/r02/ab_miller_prefetch.txt).  Since r04 off: the held line pushed the kernel to
+// 177 AGPRs and ~650 accumulator moves; without it 65 AGPRs, Miller 8.75 -> 8.30 ms
+// (profiles/r04/ab/pf_prefetch{1,0}_*.json)
 #ifndef BN_MILLER_PREFETCH
-#define BN_MILLER_PREFETCH 1
+#define BN_MILLER_PREFETCH 0
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WAVES))) void k_bn_miller(const uint32_t* __restrict__ lane_first, uint32_t nlanes,
                                                   const uint32_t* __restrict__ pidx, const uint8_t* __restrict__ pstat,
