@@ -16,10 +16,10 @@
 //     divergence), 8-entry table {1,3,...,15}R (entries 0..3 in LDS, 4..7 in per-lane scratch: the
 //     LDS of two waves per SIMD holds four), built on an isomorphic curve
 //     (libsecp-style "global z") so all table points are affine without an inversion; the lambda
-//     half uses (beta x, y).  128 doublings + 66 mixed additions (w = 3 with the 4-entry table in
+//     half uses (beta x, y).  128 doublings + 65 mixed additions (w = 3 with the 4-entry table in
 //     LDS: 129 + 88, measured 6 % slower: 15.5 -> 14.5 ms per 2^20 recoveries).
 //   * u1*G: fixed-base comb, 13 windows of 20 bits from a 1.09 GB affine table in HBM (one random
-//     80-byte entry per window, prefetched a window ahead), 13 mixed additions and no doublings
+//     80-byte entry per window, prefetched a window ahead), 12 mixed additions (window 0 starts the sum), no doublings
 //     (gsv_internal.h COMB_BITS; 16-bit windows from the Infinity Cache were 1.3 % slower).
 //   * no square root up front: u2*R runs on the curve y^2 = x^3 + 7 c^3 (c = x^3 + 7) where R is
 //     (c x, c^2); one general add to combine, carried as a + t b (t = y_R); one exponentiation by
