@@ -15,6 +15,7 @@ void h_norm_weak(uint32_t* r) { fe9 x; for (int i = 0; i < 9; i++) x.v[i] = r[i]
 int h_is_zero_weak(const uint32_t* r) { fe9 x; for (int i = 0; i < 9; i++) x.v[i] = r[i]; return fe9_is_zero_weak(x) ? 1 : 0; }
 void h_norm_full(uint32_t* r) { fe9 x; for (int i = 0; i < 9; i++) x.v[i] = r[i]; fe9_normalize_full(x); for (int i = 0; i < 9; i++) r[i] = x.v[i]; }
 void h_inv(uint32_t* r, const uint32_t* a) { fe9 x, z; for (int i = 0; i < 9; i++) x.v[i] = a[i]; fe9_inv(z, x); for (int i = 0; i < 9; i++) r[i] = z.v[i]; }
+void h_pow_pm3_4(uint32_t* r, const uint32_t* a) { fe9 x, z; for (int i = 0; i < 9; i++) x.v[i] = a[i]; fe9_pow_pm3_4(z, x); for (int i = 0; i < 9; i++) r[i] = z.v[i]; }
 int h_sqrt(uint32_t* r, const uint32_t* a) { fe9 x, z; for (int i = 0; i < 9; i++) x.v[i] = a[i]; int ok = fe9_sqrt(z, x); for (int i = 0; i < 9; i++) r[i] = z.v[i]; return ok; }
 void h_from_words(uint32_t* r, const uint32_t* w) { fe9 x; fe9_from_words(x, w); for (int i = 0; i < 9; i++) r[i] = x.v[i]; }
 void h_to_words(uint32_t* w, const uint32_t* a) { fe9 x; for (int i = 0; i < 9; i++) x.v[i] = a[i]; fe9_to_words(w, x); }

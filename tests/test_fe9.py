@@ -160,6 +160,21 @@ def test_inv_sqrt(lib):
         assert ok == 0
 
 
+def test_pow_pm3_4(lib):
+    """fe9_pow_pm3_4 (the recovery's one exponentiation, recover_dev.cuh recover_tail_twisted):
+    a^((p-3)/4), i.e. 1/sqrt(a) for a square a, on redundant inputs"""
+    rng = random.Random(17)
+    r = U9()
+    for _ in range(20):
+        x = rng.randrange(1, P)
+        lib.h_pow_pm3_4(r, arr(rnd_limbs_val(rng, x)))
+        assert val(r) % P == pow(x, (P - 3) // 4, P)
+        s = x * x % P
+        lib.h_pow_pm3_4(r, arr(from_int(s)))
+        w = val(r) % P
+        assert (w * w * s) % P == 1  # 1 / sqrt(s)^2 * s
+
+
 def rnd_limbs_val(rng, x):
     """a magnitude-2 representation of x: x + k p split with limbs up to 2^30"""
     l = from_int(x)
