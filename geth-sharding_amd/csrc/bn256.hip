@@ -713,6 +713,177 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
     fp12_store(fv, nlanes, c, f);
 }
 
+// ---- the same loop at TWO waves per SIMD (k_bn_miller_w2).  At one wave per SIMD every VALU
+// instruction holds the SIMD 4.4-5.1 cycles whatever it is (profiles/r01_microbench_lat.txt); with a
+// second wave the 43 % of the loop's instructions that are not multiply-adds cost half that.  Two waves
+// need <= 256 registers a lane (k_bn_miller: 256 + 65).  What moves out of the register file: one
+// F_p^6 value per lane in LDS ([54 words][64 lanes], conflict-free ds_read/write_b32; 13.8 KB per
+// wave, eight waves per CU = 110 KB of the 160 KB), and the F_p^6 products are computed one output
+// coordinate at a time (each coordinate one fq_dot REDC; scheduling barriers between them), so a
+// product's working set is its inputs plus one output.  The field elements are those of mul_line_i /
+// fp12_sqr_i (the same Karatsuba formulas), so the Miller values are the same F_p^12 elements.
+template <int J, class E>
+GSV_DI auto fp6_coord(const fp6t<E>& v) {  // F_p coordinate J of an F_p^6 value (x.x, x.y, y.x, y.y, z.x, z.y)
+    if constexpr (J == 0) return v.x.x;
+    else if constexpr (J == 1) return v.x.y;
+    else if constexpr (J == 2) return v.y.x;
+    else if constexpr (J == 3) return v.y.y;
+    else if constexpr (J == 4) return v.z.x;
+    else return v.z.y;
+}
+GSV_DI fq& fp6_at(fp6& v, int j) { return ((fq*)&v)[j]; }
+GSV_DI void w2_put(uint32_t* l, int j, const fq& v) {
+#pragma unroll
+    for (int w = 0; w < 9; w++) l[(j * 9 + w) * 64] = v.v[w];
+}
+GSV_DI fq w2_get(const uint32_t* l, int j) {
+    fq r;
+#pragma unroll
+    for (int w = 0; w < 9; w++) r.v[w] = l[(j * 9 + w) * 64];
+    return r;
+}
+#define W2_SEQ __builtin_amdgcn_sched_barrier(0)
+// An empty asm that "redefines" an F_p^6 value in place (no instruction): the per-coordinate products
+// below then cannot share their operand preparation (negations, xi multiples) through common-
+// subexpression elimination, which would compute them for all six coordinates up front and hold them
+// live through the whole product.
+GSV_DI void w2_opaque(fq& a) {
+    asm volatile("" : "+v"(a.v[0]), "+v"(a.v[1]), "+v"(a.v[2]), "+v"(a.v[3]), "+v"(a.v[4]), "+v"(a.v[5]), "+v"(a.v[6]),
+                 "+v"(a.v[7]), "+v"(a.v[8]));
+}
+GSV_DI void w2_opaque(fp2& a) { w2_opaque(a.x), w2_opaque(a.y); }
+GSV_DI void w2_opaque(fp6& a) { w2_opaque(a.x), w2_opaque(a.y), w2_opaque(a.z); }
+// the sparse product a (by tau + bz), one coordinate at a time: only the coordinate asked for survives
+// dead-code elimination of the fused routine
+template <int J, class B>
+GSV_DI fq w2_sparse(const fp6& a, const fp2& by, const B& bz) { return fq_store(fp6_coord<J>(fp6_mul_sparse(a, by, bz))); }
+template <int J>
+GSV_DI fq w2_dense(const fp6& a, const fp6& b) { return fq_store(fp6_coord<J>(fp6_mul(a, b))); }
+
+// mul_line_i (optate.go:94-112) with a2 = f.x (a tau + b) in LDS:
+//   a2 -> LDS;  s = f.x + f.y;  t3 = f.y c;  new.y = t3 + tau a2;
+//   d = tau a2 - a2 -> LDS;  new.x = s (a tau + b + c) - a2 - t3 = s (a tau + b + c) - new.y + d
+// The line is loaded in two parts where its coefficients are first needed (a, b; then c), so the
+// loads are not hoisted above the first products.
+GSV_DI void mul_line_w2(fp12& f, const uint32_t* __restrict__ lines, uint32_t n, uint32_t pj, int li, uint32_t* l) {
+    line L;
+    L.a = soa_load2(lines, n, pj, li * 6 + 0);
+    L.b = soa_load2(lines, n, pj, li * 6 + 2);
+    W2_SEQ;
+    w2_opaque(f.x), w2_opaque(L.a), w2_put(l, 0, w2_sparse<0>(f.x, L.a, L.b)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(L.a), w2_put(l, 1, w2_sparse<1>(f.x, L.a, L.b)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(L.a), w2_put(l, 2, w2_sparse<2>(f.x, L.a, L.b)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(L.a), w2_put(l, 3, w2_sparse<3>(f.x, L.a, L.b)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(L.a), w2_put(l, 4, w2_sparse<4>(f.x, L.a, L.b)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(L.a), w2_put(l, 5, w2_sparse<5>(f.x, L.a, L.b)); W2_SEQ;
+    L.c = soa_load2(lines, n, pj, li * 6 + 4);
+    const fp2 bc = s2(fp2_add(L.b, L.c));
+    W2_SEQ;
+    f.x = fp6_store(fp6_add(f.x, f.y));      // s
+    f.y = fp6_store(fp6_mul_fp2(f.y, L.c));  // t3
+    W2_SEQ;
+    // new.y = t3 + tau a2 = (t3.x + a2.y, t3.y + a2.z, t3.z + xi a2.x) in place, and d = tau a2 - a2 =
+    // (a2.y - a2.x, a2.z - a2.y, xi a2.x - a2.z) over a2 in LDS, in an order that holds at most two of
+    // a2's coordinates and one of d's at a time
+    {
+        fp2 a2x{w2_get(l, 0), w2_get(l, 1)}, a2y{w2_get(l, 2), w2_get(l, 3)};
+        fp2 d = s2(fp2_sub(a2y, a2x));
+        w2_put(l, 0, d.x), w2_put(l, 1, d.y);
+        const fp2 xa = s2(fp2_mul_xi(a2x));
+        f.y.x = s2(fp2_add(f.y.x, a2y));
+        W2_SEQ;
+        fp2 a2z{w2_get(l, 4), w2_get(l, 5)};
+        d = s2(fp2_sub(a2z, a2y));
+        w2_put(l, 2, d.x), w2_put(l, 3, d.y);
+        f.y.y = s2(fp2_add(f.y.y, a2z));
+        f.y.z = s2(fp2_add(f.y.z, xa));
+        d = s2(fp2_sub(xa, a2z));
+        w2_put(l, 4, d.x), w2_put(l, 5, d.y);
+    }
+    W2_SEQ;
+    // new.x = s (a tau + (b + c)) - new.y + d, coordinate by coordinate (the output replaces d in LDS)
+#define W2_NX(J)                                                                                      \
+    w2_opaque(f.x), w2_opaque(L.a);                                                                   \
+    w2_put(l, J, fq_store(fq_add(fq_sub(w2_sparse<J>(f.x, L.a, bc), fp6_at(f.y, J)), w2_get(l, J)))); \
+    W2_SEQ;
+    W2_NX(0) W2_NX(1) W2_NX(2) W2_NX(3) W2_NX(4) W2_NX(5)
+#undef W2_NX
+#pragma unroll
+    for (int j = 0; j < 6; j++) fp6_at(f.x, j) = w2_get(l, j);
+}
+// fp12_sqr_i (gfp12.go:129-143) with v0 = f.x f.y in LDS:
+//   new.x = 2 v0;  new.y = (f.x + f.y)(tau f.x + f.y) - v0 - tau v0
+GSV_DI void sqr_w2(fp12& f, uint32_t* l) {
+    w2_opaque(f.x), w2_opaque(f.y), w2_put(l, 0, w2_dense<0>(f.x, f.y)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(f.y), w2_put(l, 1, w2_dense<1>(f.x, f.y)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(f.y), w2_put(l, 2, w2_dense<2>(f.x, f.y)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(f.y), w2_put(l, 3, w2_dense<3>(f.x, f.y)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(f.y), w2_put(l, 4, w2_dense<4>(f.x, f.y)); W2_SEQ;
+    w2_opaque(f.x), w2_opaque(f.y), w2_put(l, 5, w2_dense<5>(f.x, f.y)); W2_SEQ;
+    fp6 t = fp6_store(fp6_add(fp6_mul_tau(f.x), f.y));
+    f.x = fp6_store(fp6_add(f.x, f.y));
+    W2_SEQ;
+    // new.y_J = (s t)_J - v0_J - (tau v0)_J, tau v0 = (v0.y, v0.z, xi v0.x); xi (x i + y) = (9x + y) i + (9y - x)
+    fp6 ny;
+#define W2_NY(J, TV)                                                                       \
+    w2_opaque(f.x), w2_opaque(t);                                                          \
+    fp6_at(ny, J) = fq_store(fq_sub(fq_sub(w2_dense<J>(f.x, t), w2_get(l, J)), TV)); \
+    W2_SEQ;
+    W2_NY(0, w2_get(l, 2))
+    W2_NY(1, w2_get(l, 3))
+    W2_NY(2, w2_get(l, 4))
+    W2_NY(3, w2_get(l, 5))
+    W2_NY(4, fq_add(fq_normalize(fq_mul_small<8>(w2_get(l, 0))), fq_add(w2_get(l, 0), w2_get(l, 1))))
+    W2_NY(5, fq_sub(fq_add(fq_normalize(fq_mul_small<8>(w2_get(l, 1))), w2_get(l, 1)), w2_get(l, 0)))
+#undef W2_NY
+    f.y = ny;
+#pragma unroll
+    for (int j = 0; j < 6; j++) fp6_at(f.x, j) = fq_store(fq_add(w2_get(l, j), w2_get(l, j)));
+}
+#undef W2_SEQ
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_bn_miller_w2(
+    const uint32_t* __restrict__ lane_first, uint32_t nlanes, const uint32_t* __restrict__ pidx,
+    const uint8_t* __restrict__ pstat, const uint32_t* __restrict__ lines, uint32_t npairs,
+    uint8_t* __restrict__ cstat, uint32_t* __restrict__ fv /* [108 words][nlanes] */) {
+    __shared__ uint32_t lds[54 * 64];
+    uint32_t* l = lds + threadIdx.x;
+    uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nlanes) return;
+    uint32_t b = lane_first[c], e = lane_first[c + 1];
+    bool bad = false, any = false;
+    for (uint32_t q = b; q < e; q++) {
+        uint8_t st = pstat[pidx[q]];
+        bad = bad || st == PS_BAD;
+        any = any || st == PS_OK;
+    }
+    cstat[c] = bad ? CS_BAD : any ? CS_OK : CS_ONE;
+    if (bad || !any) return;
+    fp12 f = fp12_one();
+    int li = 0;
+#pragma unroll 1
+    for (int i = 64; i > 0; i--) {
+        if (i != 64) sqr_w2(f, l);
+        uint64_t bit = 1ull << (i - 1);
+        int nl = ((NAF_POS | NAF_NEG) & bit) ? 2 : 1;
+#pragma unroll 1
+        for (uint32_t q = b; q < e; q++) {
+            uint32_t j = pidx[q];
+            if (pstat[j] != PS_OK) continue;
+#pragma unroll 1
+            for (int k = 0; k < nl; k++) mul_line_w2(f, lines, npairs, j, li + k, l);
+        }
+        li += nl;
+    }
+#pragma unroll 1
+    for (uint32_t q = b; q < e; q++) {
+        uint32_t j = pidx[q];
+        if (pstat[j] != PS_OK) continue;
+#pragma unroll 1
+        for (int k = 0; k < 2; k++) mul_line_w2(f, lines, npairs, j, li + k, l);
+    }
+    fp12_store(fv, nlanes, c, f);
+}
+
 // ---- two-lane Miller step, for batches too small to give every SIMD a wave: lanes (2c, 2c+1) run
 // Miller lane c together.  Both hold the whole accumulator; each F_p^12 squaring's two F_p^6
 // products and each line product's two sparse products (plus half of its F_p^2-scalar product)
@@ -990,14 +1161,16 @@ GSV_DI fp12 lds_fp12(const uint32_t* lds) { return fp12{lds_fp6(lds, 0), lds_fp6
 // A = ws[slot] straight from HBM into LDS (global_load_lds_dword: word q of every lane lands at
 // lds_base[q * 64 + lane], the [word][lane] layout A has), no VGPRs on the way; the data is there after
 // fe_lds_wait()
-GSV_DI void lds_fetch(uint32_t* lds_base, const uint32_t* __restrict__ ws, uint32_t n, uint32_t c, int slot) {
-    // saddr form: the workspace base in SGPRs, a 32-bit VGPR byte offset per word (< 2^32: the
-    // workspace is BN_FINAL_SLOTS x 432 bytes per check); M0 = the word's LDS row
-    const uint32_t off = ((uint32_t)slot * 108u * n + c) * 4u;
+GSV_DI void lds_fetch(uint32_t* lds_base, const uint32_t* __restrict__ ws, uint32_t n, uint32_t c0, uint32_t t,
+                      int slot) {
+    // saddr form: the row's base for the wave's first check c0 in an SGPR pair (64-bit: the workspace
+    // is BN_FINAL_SLOTS x 432 bytes per check, beyond 4 GiB above ~1.24 M checks), the lane's byte
+    // offset t * 4 (< 256) in a VGPR; M0 = the word's LDS row.  c0, n and slot are wave-uniform.
+    const uint32_t* wb = ws + (size_t)slot * 108u * n + c0;
     const uint32_t row = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)lds_base;
 #pragma unroll
     for (int q = 0; q < 108; q++)
-        asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(off + (uint32_t)q * n * 4u), "s"(ws),
+        asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(t * 4u), "s"(wb + (size_t)q * n),
                      "s"(row + (uint32_t)q * 256u)
                      : "memory", "m0");
 }
@@ -1120,7 +1293,8 @@ struct FeLane {
     uint32_t lane;
     GSV_DI FeLane() : lane(lane_id_v()) {}
     GSV_DI uint32_t t() const { return COOP ? lane / 3 : lane; }
-    GSV_DI uint32_t check() const { return blockIdx.x * (COOP ? FINAL3_PER_WAVE : 64u) + t(); }
+    GSV_DI uint32_t check0() const { return blockIdx.x * (COOP ? FINAL3_PER_WAVE : 64u); }  // wave-uniform
+    GSV_DI uint32_t check() const { return check0() + t(); }
     GSV_DI int role() const { return COOP ? (int)(lane - 3 * t()) : 0; }
     GSV_DI int base() const { return COOP ? (int)(3 * t()) : -1; }
 };
@@ -1155,7 +1329,7 @@ GSV_DI fp12 final_exp_run(fp12 X, const FinalArgs& fa, uint32_t* lds_base, uint3
         }
         case FE_CSQR:
         case FE_CSQR_LDA: {
-            if (k == FE_CSQR_LDA) lds_fetch(lds_base, fa.ws, fa.nchecks, ln.check(), (int)slot);
+            if (k == FE_CSQR_LDA) lds_fetch(lds_base, fa.ws, fa.nchecks, ln.check0(), ln.t(), (int)slot);
             if constexpr (COOP) {
                 fp12 m;
                 fp12_cyclo_sqr3_i(&m, X, ln.role(), ln.base());
@@ -1178,7 +1352,7 @@ GSV_DI fp12 final_exp_run(fp12 X, const FinalArgs& fa, uint32_t* lds_base, uint3
             break;
         }
         case FE_LDX: X = ws_load(fa.ws, fa.nchecks, ln.check(), (int)slot); break;
-        case FE_LDA: lds_fetch(lds_base, fa.ws, fa.nchecks, ln.check(), (int)slot); break;
+        case FE_LDA: lds_fetch(lds_base, fa.ws, fa.nchecks, ln.check0(), ln.t(), (int)slot); break;
         case FE_STX: ws_store(fa.ws, fa.nchecks, ln.check(), (int)slot, X); break;
         case FE_LDFV: lds_put(lds, fv_extra(fa, ln.check(), pc >> 1)); break;
         default: break;
@@ -1488,6 +1662,9 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
         if (layout & GSV_BN_LAYOUT_MILLER2)
             hipLaunchKernelGGL(bn::k_bn_miller2, dim3((2 * nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
+                               d_pidx, d_use, d_lines, npairs, d_lstat, d_fv);
+        else if (layout & GSV_BN_LAYOUT_MILLERW2)
+            hipLaunchKernelGGL(bn::k_bn_miller_w2, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
                                d_pidx, d_use, d_lines, npairs, d_lstat, d_fv);
         else
             hipLaunchKernelGGL(bn::k_bn_miller, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,

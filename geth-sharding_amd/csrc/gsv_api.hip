@@ -836,6 +836,12 @@ bool bn_conc(size_t npairs, int cus) {
     if (!gsv::bn256_layout_forks()) return true;
     return npairs <= (size_t)std::max(cus, 1) * 4 * 64 * 1;
 }
+// The Miller loop at two waves per SIMD (k_bn_miller_w2: one F_p^6 value per lane in LDS, products one
+// output coordinate at a time) or at one (k_bn_miller).  GSV_BN_MILLER_W2 = 0/1 forces the choice.
+bool bn_miller_w2() {
+    if (const char* e = getenv("GSV_BN_MILLER_W2")) return atoi(e) != 0;
+    return true;
+}
 // Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
 // lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
 // and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
@@ -848,7 +854,7 @@ uint32_t bn_pairs_per_lane(size_t np, int cus, int depth) {
         int k = atoi(e);
         if (k >= 1) return (uint32_t)k;
     }
-    const size_t waves = 1;
+    const size_t waves = bn_miller_w2() ? 2 : 1;  // Miller waves per SIMD the kernel's registers admit
     size_t target = (size_t)std::max(cus, 1) * 4 * 64 * waves / (depth >= 3 ? 6 : 1);
     for (uint32_t k = 4; k > 1; k >>= 1)
         if ((np + k - 1) / k >= target) return k;
@@ -865,8 +871,9 @@ std::vector<uint64_t> pairing_key(const uint64_t* h_off, size_t n) {
     const char* f = getenv("GSV_BN_FINAL3");
     const char* m = getenv("GSV_BN_MILLER2");
     const char* cc = getenv("GSV_BN_CONC");
+    const char* w2 = getenv("GSV_BN_MILLER_W2");
     std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0, m ? (uint64_t)atoi(m) + 1 : 0,
-                              cc ? (uint64_t)atoi(cc) + 1 : 0};
+                              cc ? (uint64_t)atoi(cc) + 1 : 0, w2 ? (uint64_t)atoi(w2) + 1 : 0};
     key.insert(key.end(), h_off, h_off + n + 1);
     return key;
 }
@@ -935,7 +942,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.deep = depth >= 3;
     s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
                (bn_miller2(s.nl, cus, depth) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
-               (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0);
+               (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0) | (bn_miller_w2() ? gsv::GSV_BN_LAYOUT_MILLERW2 : 0);
     s.o_src = L.add(np * 8 + 8);
     s.o_pidx = L.add(np * 4 + 4);
     s.o_lfirst = L.add((s.nl + 1) * 4);

@@ -142,6 +142,33 @@ def test_pairing_dev_prepared_at_depth_three(ctx, oracle):
         assert (got == want).all(), [(i, int(got[i]), int(want[i])) for i in np.nonzero(got != want)[0]]
 
 
+@pytest.mark.parametrize("final3", ["0", "1"])
+def test_pairing_workspace_beyond_4gib(ctx, monkeypatch, final3):
+    """1,300,000 checks: the final exponentiation's workspace (8 x 432 bytes per check, 4.5 GB) spans
+    more than 2^32 bytes, so its HBM -> LDS fetches must address 64-bit (a 32-bit offset
+    wrapped above ~1.24 M checks).  All but the last 1,024 checks are empty (true, final exponentiation
+    of 1); the last 1,024 are configs[4]-generator checks whose expected verdicts the generator gives
+    (tied to the oracle by test_synth_checks_match_oracle) — their workspace rows sit highest."""
+    import torch
+    monkeypatch.setenv("GSV_BN_FINAL3", final3)
+    n, m = 1_300_000, 1024
+    dev = torch.device("cuda", ctx.device)
+    pin = torch.empty((m, 768), dtype=torch.uint8, device=dev)
+    exp = torch.empty((m,), dtype=torch.uint8, device=dev)
+    ctx.bn256_synth_checks_dev(91, pin, exp)
+    torch.cuda.synchronize()
+    off = np.zeros(n + 1, np.uint64)
+    off[n - m + 1:] = np.arange(1, m + 1, dtype=np.uint64) * 768
+    ver = torch.full((n,), 9, dtype=torch.uint8, device=dev)
+    ctx.pairing_check_batch_dev(pin.reshape(-1), off, ver)
+    torch.cuda.synchronize()
+    got = ver.cpu().numpy()
+    assert (got[:n - m] == 1).all(), np.nonzero(got[:n - m] != 1)[0][:10]
+    e = exp.cpu().numpy()
+    assert (got[n - m:] == e).all(), np.nonzero(got[n - m:] != e)[0][:10]
+    assert set(e.tolist()) == {0, 1, 2}
+
+
 def test_pairing_empty_batch_and_empty_input(ctx):
     assert ctx.pairing_check_batch([]).shape == (0,)
     assert ctx.pairing_check_batch([b""])[0] == 1  # empty input -> true32Byte

@@ -20,7 +20,8 @@ def emu(tmp_path_factory, oracle):
     if not os.path.exists(os.path.join(LIBDIR, "libgsv.so")):
         pytest.skip("libgsv.so not built")
     out = tmp_path_factory.mktemp("planemu") / "plan_emu.so"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", str(out),
+    from conftest import SANITIZE_FLAGS  # ASan/UBSan under tools/sanitize.sh
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC"] + SANITIZE_FLAGS + ["-o", str(out),
                     os.path.join(ROOT, "tests", "native", "plan_emu.cpp"),
                     "-L" + LIBDIR, "-lgsv", "-Wl,-rpath," + LIBDIR,
                     "-L" + os.path.join(ROOT, "oracle"), "-l:liboracle.so", "-Wl,-rpath," + os.path.join(ROOT, "oracle")],

@@ -67,6 +67,36 @@ __global__ __launch_bounds__(256) void k_occ(uint32_t* out, uint32_t seed) {
                          : "+v"(a9.v[0]), "+v"(a9.v[1]), "+v"(a9.v[2]), "+v"(a9.v[3]), "+v"(a9.v[4]), "+v"(a9.v[5]),
                            "+v"(a9.v[6]), "+v"(a9.v[7])
                          : "v"(y0));
+        } else if (MODE >= 10 && MODE <= 17) {  // 32-bit bit ops of the Keccak rounds and their alternatives
+#define OP8(ins) asm volatile(R4(ins " %0, %0, %8, %9\n\t" ins " %1, %1, %8, %9\n\t" ins " %2, %2, %8, %9\n\t"   \
+                                     ins " %3, %3, %8, %9\n\t" ins " %4, %4, %8, %9\n\t" ins " %5, %5, %8, %9\n\t"   \
+                                     ins " %6, %6, %8, %9\n\t" ins " %7, %7, %8, %9\n\t")                             \
+                              : "+v"(a9.v[0]), "+v"(a9.v[1]), "+v"(a9.v[2]), "+v"(a9.v[3]), "+v"(a9.v[4]),        \
+                                "+v"(a9.v[5]), "+v"(a9.v[6]), "+v"(a9.v[7])                                       \
+                              : "v"(y0), "v"(y1))
+#define OP8_2(ins) asm volatile(R4(ins " %0, %0, %8\n\t" ins " %1, %1, %8\n\t" ins " %2, %2, %8\n\t"             \
+                                     ins " %3, %3, %8\n\t" ins " %4, %4, %8\n\t" ins " %5, %5, %8\n\t"             \
+                                     ins " %6, %6, %8\n\t" ins " %7, %7, %8\n\t")                                   \
+                              : "+v"(a9.v[0]), "+v"(a9.v[1]), "+v"(a9.v[2]), "+v"(a9.v[3]), "+v"(a9.v[4]),        \
+                                "+v"(a9.v[5]), "+v"(a9.v[6]), "+v"(a9.v[7])                                       \
+                              : "v"(y0))
+            if (MODE == 10) OP8_2("v_xor_b32_e32");
+            else if (MODE == 11) OP8_2("v_xor_b32_e64");
+            else if (MODE == 12) {
+                asm volatile(R4("v_bitop3_b32 %0, %0, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %9 bitop3:0x96\n\t"
+                                "v_bitop3_b32 %2, %2, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %3, %3, %8, %9 bitop3:0x96\n\t"
+                                "v_bitop3_b32 %4, %4, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %5, %5, %8, %9 bitop3:0x96\n\t"
+                                "v_bitop3_b32 %6, %6, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %7, %7, %8, %9 bitop3:0x96\n\t")
+                             : "+v"(a9.v[0]), "+v"(a9.v[1]), "+v"(a9.v[2]), "+v"(a9.v[3]), "+v"(a9.v[4]), "+v"(a9.v[5]),
+                               "+v"(a9.v[6]), "+v"(a9.v[7])
+                             : "v"(y0), "v"(y1));
+            } else if (MODE == 13) OP8("v_or3_b32");
+            else if (MODE == 14) OP8("v_bfi_b32");
+            else if (MODE == 15) OP8("v_perm_b32");
+            else if (MODE == 16) OP8("v_alignbyte_b32");
+            else OP8("v_add3_u32");
+#undef OP8
+#undef OP8_2
         } else if (MODE == 9) {  // the mul's mix: 4 mads + 1 64-bit shift + 1 and, dependent as in a column
             asm volatile(R4("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_mad_u64_u32 %0, vcc, %3, %2, %0\n\t"
                             "v_mad_u64_u32 %0, vcc, %2, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %3, %0\n\t"
@@ -100,6 +130,9 @@ int main() {
         {"v_mad_u64_u32 x8 indep", k_occ<3>, 32}, {"v_add_u32 x8 indep", k_occ<4>, 32},
         {"v_lshrrev_b64 x8 indep", k_occ<6>, 32}, {"v_alignbit_b32 x8 indep", k_occ<7>, 32},
         {"v_and_b32 lit x8 indep", k_occ<8>, 32}, {"mad/lshr64 dep chain", k_occ<9>, 32},
+        {"v_xor_b32 (VOP2) x8", k_occ<10>, 32}, {"v_xor_b32_e64 (VOP3) x8", k_occ<11>, 32},
+        {"v_bitop3_b32 x8", k_occ<12>, 32}, {"v_or3_b32 x8", k_occ<13>, 32}, {"v_bfi_b32 x8", k_occ<14>, 32},
+        {"v_perm_b32 x8", k_occ<15>, 32}, {"v_alignbyte_b32 x8", k_occ<16>, 32}, {"v_add3_u32 x8", k_occ<17>, 32},
     };
     for (auto& k : ks) CHECK(hipFuncSetAttribute((const void*)k.f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     int rounds = 16;
