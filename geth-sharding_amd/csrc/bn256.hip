@@ -618,13 +618,9 @@ enum : uint8_t { CS_OK = 0, CS_BAD = 1, CS_ONE = 2 };  // CS_ONE: no finite pair
 #ifndef BN_MILLER_WAVES
 #define BN_MILLER_WAVES 1
 #endif
-// 1: k_bn_miller loads each line one multiplication ahead (r02: Miller 9.0 -> 8.8 ms at 65,536
-// checks, profiles/r02/ab_miller_prefetch.txt).  Since r04 off: the held line pushed the kernel to
-// 177 AGPRs and ~650 accumulator moves; without it 65 AGPRs, Miller 8.75 -> 8.30 ms
-// (profiles/r04/ab/pf_prefetch{1,0}_*.json)
-#ifndef BN_MILLER_PREFETCH
-#define BN_MILLER_PREFETCH 0
-#endif
+// (Through r04 a BN_MILLER_PREFETCH form loaded each line one multiplication ahead; the held line cost
+// 177 AGPRs and ~650 accumulator moves, and without it the Miller kernel ran 8.75 -> 8.30 ms at 65,536
+// checks, profiles/r04/ab/pf_prefetch{1,0}_*.json.  Unused since, removed in r05.)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WAVES))) void k_bn_miller(const uint32_t* __restrict__ lane_first, uint32_t nlanes,
                                                   const uint32_t* __restrict__ pidx, const uint8_t* __restrict__ pstat,
                                                   const uint32_t* __restrict__ lines, uint32_t npairs,
@@ -642,52 +638,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
     cstat[c] = bad ? CS_BAD : any ? CS_OK : CS_ONE;
     if (bad || !any) return;
     fp12 f = fp12_one();
-#if BN_MILLER_PREFETCH
-    {
-    // the lane's valid pairs, then one flat walk over (step, pair, line) that loads the next line
-    // while the current one is multiplied in (one wave per SIMD: nothing else hides the load latency)
-    uint32_t jv[4];
-    int m = 0;
-    for (uint32_t q = b; q < e && m < 4; q++) {
-        uint32_t j = pidx[q];
-        if (pstat[j] == PS_OK) jv[m++] = j;
-    }
-    // every lane walks the wave's largest pair count mw (a lane with fewer finite pairs, e.g. an
-    // infinity pair skipped, idles through the extra line products): the squarings at the step
-    // boundaries then stay wave-uniform instead of running once per distinct pair count
-    const int mw = __ballot(m >= 4) ? 4 : __ballot(m >= 3) ? 3 : __ballot(m >= 2) ? 2 : 1;
-    for (int t = m; t < 4; t++) jv[t] = jv[0];
-    auto nl_of = [](int i) { return i == 0 || (((NAF_POS | NAF_NEG) >> (i - 1)) & 1ull) ? 2 : 1; };
-    line cur = line_load(lines, npairs, jv[0], 0);
-    int i = 64, q = 0, k = 0, li = 0;  // step i = 64..1 (the loop), 0 = the two Frobenius lines
-#pragma unroll 1
-    while (true) {
-        int ni = i, nq = q, nk = k + 1, nli = li;
-        if (nk >= nl_of(i)) {
-            nk = 0;
-            nq = q + 1;
-            if (nq >= mw) {
-                nq = 0;
-                nli = li + nl_of(i);
-                ni = i - 1;
-            }
-        }
-        bool more = ni >= 0;
-        line nxt = cur;
-        if (more) nxt = line_load(lines, npairs, jv[nq], nli + nk);
-        if (q < m) mul_line_i(f, cur);
-        if (!more) break;
-        if (ni != i && ni != 0) f = fp12_sqr_i(f);
-        cur = nxt;
-        i = ni;
-        q = nq;
-        k = nk;
-        li = nli;
-    }
-    fp12_store(fv, nlanes, c, f);
-    return;
-    }
-#endif
     int li = 0;
 #pragma unroll 1
     for (int i = 64; i > 0; i--) {
@@ -713,7 +663,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
     fp12_store(fv, nlanes, c, f);
 }
 
-// ---- the same loop at TWO waves per SIMD (k_bn_miller_w2).  At one wave per SIMD every VALU
+// ---- the same loop at TWO waves per SIMD (k_bn_miller_w2; GSV_BN_MILLER_W2 = 1, not the default: it
+// measured slower, r05 — at 65,536 checks k = 2 11.2 vs 9.8 ms of Miller and k = 4 17.0 vs 8.3 ms,
+// profiles/r05/ab/miller_w2_sweep_*.txt: the per-coordinate form runs 10.5 k instead of 8.8 k VALU
+// instructions per line product, and at two waves the LDS round trips and line loads stay exposed).  At one wave per SIMD every VALU
 // instruction holds the SIMD 4.4-5.1 cycles whatever it is (profiles/r01_microbench_lat.txt); with a
 // second wave the 43 % of the loop's instructions that are not multiply-adds cost half that.  Two waves
 // need <= 256 registers a lane (k_bn_miller: 256 + 65).  What moves out of the register file: one

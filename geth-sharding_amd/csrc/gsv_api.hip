@@ -837,10 +837,14 @@ bool bn_conc(size_t npairs, int cus) {
     return npairs <= (size_t)std::max(cus, 1) * 4 * 64 * 1;
 }
 // The Miller loop at two waves per SIMD (k_bn_miller_w2: one F_p^6 value per lane in LDS, products one
-// output coordinate at a time) or at one (k_bn_miller).  GSV_BN_MILLER_W2 = 0/1 forces the choice.
+// output coordinate at a time) or at one (k_bn_miller, the default).  The two-wave kernel measured
+// slower at every batch size (r05: 65,536 checks at k = 2 11.2 vs 9.8 ms of Miller, k = 4 17.0 vs
+// 8.3 ms; 8,192 checks three deep 4.7 vs 3.75 ms per batch, profiles/r05/ab/miller_w2_sweep_*.txt):
+// 19 % more VALU per line product and exposed LDS / line-load latency outweigh the second wave.
+// GSV_BN_MILLER_W2 = 1 selects it (A/B and its GPU test).
 bool bn_miller_w2() {
     if (const char* e = getenv("GSV_BN_MILLER_W2")) return atoi(e) != 0;
-    return true;
+    return false;
 }
 // Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
 // lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,

@@ -251,38 +251,37 @@ GSV_DI void gtab_load(ge9& P, const uint4* e) {
     }
 }
 
-// window w's digit of the 256-bit scalar u: bits [COMB_BITS w, COMB_BITS (w + 1)), which may straddle
-// two limbs (bits past 255 are 0)
-GSV_DI uint32_t comb_digit(const sc& u, uint32_t w) {
-    constexpr uint32_t MASK = (1u << COMB_BITS) - 1u;
-    if constexpr (32 % COMB_BITS == 0) {
-        constexpr uint32_t PER = 32 / COMB_BITS;
-        return (sel_word(u.v, w / PER) >> ((w % PER) * COMB_BITS)) & MASK;
-    } else {
-        const uint32_t x[9] = {u.v[0], u.v[1], u.v[2], u.v[3], u.v[4], u.v[5], u.v[6], u.v[7], 0u};
-        uint32_t bit = w * (uint32_t)COMB_BITS, k = bit >> 5, sh = bit & 31u;
-        uint64_t pair = ((uint64_t)sel_word(x, k + 1) << 32) | sel_word(x, k);
-        return (uint32_t)(pair >> sh) & MASK;
-    }
+// the scalar shifted right by COMB_BITS in place (8 words; v_alignbit pairs)
+GSV_DI void comb_shift(uint32_t c[8]) {
+#pragma unroll
+    for (int i = 0; i < 7; i++) c[i] = __builtin_amdgcn_alignbit(c[i + 1], c[i], COMB_BITS);
+    c[7] >>= COMB_BITS;
 }
-
-// u*G with the fixed-base comb table (COMB_WINDOWS mixed adds, no doublings)
+// u*G with the fixed-base comb table (COMB_WINDOWS mixed adds, no doublings).  The windows' digits are
+// read from the bottom of a copy of u shifted by COMB_BITS per window (r05): comb_digit's word select
+// with a loop-variant index was turned into a private array written to scratch and read back by a
+// dynamic offset twice per window (72 bytes of scratch stores per window, ~0.8 KB per recovery; r04's
+// 0.78 GB of writes per 2^20-recovery launch).
 GSV_DI void comb_mul_g9(gej9& acc, bool& inf, const sc& u, const uint4* __restrict__ gtab) {
+    constexpr uint32_t MASK = (1u << COMB_BITS) - 1u;
+    uint32_t c[8] = {u.v[0], u.v[1], u.v[2], u.v[3], u.v[4], u.v[5], u.v[6], u.v[7]};
     ge9 Pn;
-    gtab_load(Pn, gtab + (size_t)comb_digit(u, 0) * GTAB_ENTRY_U4);
+    const uint32_t d0 = c[0] & MASK;
+    gtab_load(Pn, gtab + (size_t)d0 * GTAB_ENTRY_U4);
     // window 0 starts the sum: its entry is the accumulator (Z = 1), no add
     acc.x = Pn.x;
     acc.y = Pn.y;
     fe9_set_u32(acc.z, 1);
-    inf = comb_digit(u, 0) == 0;
-    gtab_load(Pn, gtab + (((size_t)1 << COMB_BITS) + comb_digit(u, 1)) * GTAB_ENTRY_U4);
+    inf = d0 == 0;
+    comb_shift(c);  // c = u >> (COMB_BITS w) at the top of window w
+    gtab_load(Pn, gtab + (((size_t)1 << COMB_BITS) + (c[0] & MASK)) * GTAB_ENTRY_U4);
 #pragma unroll 1
     for (int w = 1; w < COMB_WINDOWS; w++) {
-        uint32_t d = comb_digit(u, (uint32_t)w);
+        uint32_t d = c[0] & MASK;
         ge9 P = Pn;
         if (w < COMB_WINDOWS - 1) {  // prefetch next window's entry
-            uint32_t dn = comb_digit(u, (uint32_t)w + 1);
-            gtab_load(Pn, gtab + (((size_t)(w + 1) << COMB_BITS) + dn) * GTAB_ENTRY_U4);
+            comb_shift(c);
+            gtab_load(Pn, gtab + (((size_t)(w + 1) << COMB_BITS) + (c[0] & MASK)) * GTAB_ENTRY_U4);
         }
         gej9 t;
         bool tinf = inf;

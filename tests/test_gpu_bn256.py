@@ -102,6 +102,58 @@ def test_pairing_miller_lane_split(ctx, oracle, monkeypatch, k):
     assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
 
 
+@pytest.mark.parametrize("k", [1, 2, 4])
+def test_pairing_two_wave_miller(ctx, oracle, monkeypatch, k):
+    """k_bn_miller_w2 (GSV_BN_MILLER_W2 = 1: one F_p^6 value per lane in LDS, products one output
+    coordinate at a time; not the default) gives the oracle's verdicts at every split."""
+    monkeypatch.setenv("GSV_BN_MILLER_W2", "1")
+    monkeypatch.setenv("GSV_BN_MILLER2", "0")
+    monkeypatch.setenv("GSV_BN_PAIRS_PER_LANE", str(k))
+    inputs = _random_inputs(oracle, 71 + k)
+    out = ctx.pairing_check_batch(inputs)
+    want = np.array([_v(oracle, x) for x in inputs], np.uint8)
+    assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
+
+
+@pytest.mark.parametrize("layout", ["auto", "k1", "k2", "k4", "final3", "final1", "miller2", "w2"])
+def test_configs4_rank_batch_depth_three(ctx, monkeypatch, layout):
+    """The N = 8 per-rank share of configs[4]: 8,192 checks from the configs[4] generator (seed 5000, all
+    six seeded classes: G1 / G2 infinity pairs, (inf, outside-G2 Q), (inf, off-twist Q), a pair with Q
+    outside G2, coordinate == p, and the perturbed false checks), prepared at pipeline depth 3 and run
+    on three streams as bench.py runs it, under the auto layout and each forced one.  Verdicts must
+    equal the generator's expectation (which test_configs4_full_batch_verdicts ties to the oracle)."""
+    import torch
+    env = {"k1": ("GSV_BN_PAIRS_PER_LANE", "1"), "k2": ("GSV_BN_PAIRS_PER_LANE", "2"),
+           "k4": ("GSV_BN_PAIRS_PER_LANE", "4"), "final3": ("GSV_BN_FINAL3", "1"),
+           "final1": ("GSV_BN_FINAL3", "0"), "miller2": ("GSV_BN_MILLER2", "1"), "w2": ("GSV_BN_MILLER_W2", "1")}
+    if layout in env:
+        monkeypatch.setenv(*env[layout])
+    n = 8192
+    dev = torch.device("cuda", ctx.device)
+    pin = torch.empty((n, 768), dtype=torch.uint8, device=dev)
+    exp = torch.empty((n,), dtype=torch.uint8, device=dev)
+    ctx.bn256_synth_checks_dev(5000, pin, exp)
+    torch.cuda.synchronize()
+    e = exp.cpu().numpy()
+    assert (e == 2).sum() == 32 and (e == 0).sum() == 1016  # 4 bad-input classes x 8 groups; false checks
+    off = np.arange(n + 1, dtype=np.uint64) * 768
+    ctx.set_pipeline_depth(3)
+    try:
+        ctx.pairing_prepare(off)
+    finally:
+        ctx.set_pipeline_depth(1)
+    ss = [torch.cuda.Stream(device=dev) for _ in range(3)]
+    outs = [torch.full((n,), 9, dtype=torch.uint8, device=dev) for _ in range(6)]
+    for s_ in ss:
+        s_.wait_stream(torch.cuda.current_stream())
+    for i, o in enumerate(outs):
+        ctx.pairing_check_batch_dev(pin, off, o, stream=ss[i % 3], prepare=False)
+    torch.cuda.synchronize()
+    for o in outs:
+        got = o.cpu().numpy()
+        assert (got == e).all(), [(i, int(got[i]), int(e[i])) for i in np.nonzero(got != e)[0][:10]]
+
+
 @pytest.mark.parametrize("k,miller2", [(1, "0"), (1, "1"), (2, "0"), (2, "1")])
 def test_pairing_two_lane_miller_on_off(ctx, oracle, monkeypatch, k, miller2):
     """The two-lane Miller step (small batches at pipeline depth <= 2) and the one-lane loop (what a

@@ -86,6 +86,11 @@ def run_pipelined(ctx, n, depth, steps=12):
         ctx.pairing_check_batch_dev(pin, off, pv[i], stream=ss[i], prepare=False)
     torch.cuda.synchronize()
     assert all(torch.equal(v, pexp) for v in pv), "verdicts differ from the constructed truth"
+    # warm-up at full depth before timing (a fresh process's first batches read ~1.4x slow: clocks and
+    # first-use costs; r04/r05 sweeps that timed the first depth of a process carried that artifact)
+    for i in range(4 * depth):
+        ctx.pairing_check_batch_dev(pin, off, pv[i % depth], stream=ss[i % depth], prepare=False)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
         ctx.pairing_check_batch_dev(pin, off, pv[i % depth], stream=ss[i % depth], prepare=False)

@@ -87,6 +87,11 @@ def main(root):
                 r["gpu_cycles_per_dispatch"] = round(gui / 8)
                 if r.get("avg_ms"):  # effective clock of the profiled run (MI355X_MICROARCH.md, DVFS)
                     r["profiled_clock_ghz"] = round(gui / 8 / (r["avg_ms"] * 1e6), 3)
+            if wcyc and gui:
+                # achieved occupancy: SQ_WAVE_CYCLES sums every resident wave's lifetime in quad-cycles
+                # (MI355X_MICROARCH.md, cycle constants), so x 4 over the 1,024 SIMDs' cycles = the mean
+                # number of resident waves per SIMD over the dispatch
+                r["mean_waves_per_simd"] = round(wcyc * 4 / (1024 * gui / 8), 3)
             if wcyc:  # where the waves' cycles went (disjoint buckets, quad-cycle units)
                 for key, name in (("SQ_WAIT_ANY", "wait_any_frac"), ("SQ_WAIT_INST_ANY", "wait_inst_any_frac"),
                                   ("SQ_ACTIVE_INST_ANY", "active_inst_any_frac")):
