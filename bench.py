@@ -53,17 +53,28 @@ FP_MULS_PER_CHECK_REF = 106852            # tests/test_oracle.py pins the figure
 MACS_PER_FP_MUL = 128                      # Montgomery product: 64 + 64 partial products
 PERMS_PER_MIB = 83016                      # Keccak-f permutations per 1 MiB chunk root (data-independent)
 # The Keccak-f[1600] instruction floor on 32-bit VALU (fixed, not the measured count, so instruction
-# bloat shows in `frac`): per round, theta's column parities 2 v_xor3 per half-column (20), rot(C, 1)
-# 2 v_alignbit per column (10), A ^= C[x-1] ^ rot(C[x+1]) one v_xor3 per word (50); rho 2 v_alignbit
-# per rotated lane (48); chi one v_bitop3 per word (50); iota 2 v_xor: 180 per round, 24 rounds.
+# bloat shows in `frac`): per round, theta's column parities 2 three-input XORs per half-column (20),
+# rot(C, 1) 2 v_alignbit per column (10), A ^= C[x-1] ^ rot(C[x+1]) one three-input XOR per word (50);
+# rho 2 v_alignbit per rotated lane (48); chi one v_bitop3 per word (50); iota 2 v_xor: 180 per round,
+# 24 rounds.  (gfx950's assembler has no v_xor3_b32: a three-input XOR is v_bitop3_b32 with table 0x96.)
 KECCAK_VALU_FLOOR_PER_PERM = 24 * 180
-# Peaks (profiles/r02/microbench_{int,lat}.txt, tools/microbench_*.hip on MI355X):
+# The same permutation priced by what each instruction costs on the SIMD (r05,
+# profiles/r05/microbench_occ_ops.txt, tools/microbench_occ.hip: SIMD-cycles per wave64 instruction at
+# four waves per SIMD, nominal 2.4 GHz): v_bitop3_b32 2.31 and v_xor_b32 2.37 issue at the full rate,
+# v_alignbit_b32 (like every other three-source VALU op measured: v_or3, v_add3, v_bfi, v_perm,
+# v_alignbyte) at half, 4.22.  The compiled round is 70 v_bitop3 + 62 v_xor + 58 v_alignbit
+# (ISA of k_chunk_level<BOTTOM>), so a permutation holds a SIMD >= 24 x 553 cycles: the `frac_mix_ceiling`
+# denominator, the rate a kernel doing nothing but this round could reach.
+KECCAK_ROUND_MIX = {"v_bitop3_b32": (70, 2.31), "v_xor_b32": (62, 2.37), "v_alignbit_b32": (58, 4.22)}
+KECCAK_MIX_CYCLES_PER_PERM = 24 * sum(n * c for n, c in KECCAK_ROUND_MIX.values())
+# Peaks (tools/microbench_{int,lat,occ}.hip on MI355X: profiles/r01_microbench_int.txt,
+# profiles/r05/microbench_occ_ops.txt):
 #   VALU issue: CDNA4 SIMDs are 32 wide, a wave64 instruction issues over 2 cycles -> at most 0.5
 #   wave-instructions per SIMD per cycle (MI355X_MICROARCH.md, cdna_hip_programming.md §CDNA4).
 #   v_mad_u64_u32 (and every carry / 64-bit op) issues at a quarter of the 64-lane rate: 16
-#   lanes/clk/SIMD = 4 cycles per wave-instruction; 4.43 cycles measured with two waves per SIMD,
+#   lanes/clk/SIMD = 4 cycles per wave-instruction; 4.17-4.29 measured at 2-8 waves per SIMD (r05),
 #   and more waves do not raise it (k_ecrecover at 2, 3 and 4 waves/SIMD: 15.46 / 15.32 / 15.71 ms,
-#   profiles/r02/ab_ecrecover_occupancy.txt).
+#   profiles/r02/ab_ecrecover_occupancy.txt, re-measured r04: profiles/r04/ab/w3_*.json).
 VALU_ISSUE_PEAK = 0.5
 PEAK_LANE_OPS = SIMDS * 64 * VALU_ISSUE_PEAK * CLOCK          # 7.86e13 full-rate 32-bit lane-ops/s
 PEAK_MAC = SIMDS * 16 * CLOCK                                 # 3.93e13 v_mad_u64_u32 lane-ops/s
@@ -110,9 +121,21 @@ def clock_fracs(units_per_launch, k, peak_units_per_s):
     return out
 
 
+def mix_ceiling(units_per_launch, ms):
+    """The Keccak legs against the permutation's issue-cost ceiling (KECCAK_MIX_CYCLES_PER_PERM: the
+    compiled round's instructions at their measured SIMD cycles), beside the fixed instruction floor."""
+    peak = SIMDS * 64 * CLOCK / KECCAK_MIX_CYCLES_PER_PERM
+    out = {"mix_ceiling": round(peak / 1e9, 3), "mix_cycles_per_permutation": round(KECCAK_MIX_CYCLES_PER_PERM),
+           "mix_basis": "24 rounds x (70 v_bitop3 x 2.31 + 62 v_xor x 2.37 + 58 v_alignbit x 4.22) SIMD-cycles, "
+                        "profiles/r05/microbench_occ_ops.txt"}
+    if ms:
+        out["frac_mix_ceiling"] = round(units_per_launch / (ms * 1e-3) / peak, 4)
+    return out
+
+
 def opcount(unit):
     """Field products per unit counted by the instrumented build (tools/count_ops.py ->
-    profiles/r02/opcount.json): {"mac_equiv": ..., ...} or None."""
+    profiles/<round>/opcount.json): {"mac_equiv": ..., ...} or None."""
     d = _profile("opcount.json") or {}
     return d.get(unit)
 
@@ -451,7 +474,8 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
                           "permutation (the fixed Keccak-f floor, bench.py KECCAK_VALU_FLOOR_PER_PERM)",
             "valu_instr_per_permutation": round(ipp, 1) if ipp else None,
             "valu_instr_over_floor": round(ipp / KECCAK_VALU_FLOOR_PER_PERM, 3) if ipp else None,
-            **clock_fracs(bot_perms, k, ceiling),
+            **clock_fracs(bot_perms, k, ceiling), **mix_ceiling(bot_perms, bot_ms),
+            "mean_waves_per_simd": k.get("mean_waves_per_simd"),
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
             # the body bytes read + every bottom node's raw 32-byte hash written into its parent's slot
             "traffic": traffic, "algorithmic_bytes_per_launch": N_SHARDS * BODY + bot_perms * 32,
@@ -659,7 +683,8 @@ def leg_keccak(ctx, stream, dev, ws, rank, args):
                           f"{KECCAK_VALU_FLOOR_PER_PERM} VALU instructions per permutation)",
             "valu_instr_per_permutation": round(ipp, 1) if ipp else None,
             "valu_instr_over_floor": round(ipp / KECCAK_VALU_FLOOR_PER_PERM, 3) if ipp else None,
-            **clock_fracs(perms, k, ceiling),
+            **clock_fracs(perms, k, ceiling), **mix_ceiling(perms, kavg),
+            "mean_waves_per_simd": k.get("mean_waves_per_simd"),
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
             "traffic": traffic, "algorithmic_bytes_per_launch": int(voff[-1]) + (nblk * ntx + 1) * 8 + nblk * ntx * 32,
             "hbm_GBps": round(traffic / (k["avg_ms"] * 1e-3) / 1e9, 1) if traffic and k.get("avg_ms") else None,
@@ -807,6 +832,8 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     oc = opcount("pairing_check")
     act = oc["mac_equiv"] * nloc / (k_tot * 1e-3) if oc else None
     kk = {n: pmc(f"gsv::bn::{n}", "pmc_pairing.json") for n in ("k_bn_lines", "k_bn_miller", "k_bn_final")}
+    if not kk["k_bn_lines"]:  # the two-wave lines kernel (large batches, r05)
+        kk["k_bn_lines"] = pmc("gsv::bn::k_bn_lines_w2", "pmc_pairing.json")
     # headline = the v_mad_u64_u32 our kernels execute (frac_actual).  The reference algorithm's work
     # (its 254-bit Order*Q subgroup check included, which this path replaces by three psi maps on the
     # line chain's final point) is reported only as a work ratio, not as a roofline fraction
@@ -999,6 +1026,8 @@ def main():
                "threads": info["threads_all_core"],
                "threads_basis": "one host thread per CPU of one GPU's share of an 8-GPU node (nproc / 8)",
                "cgroup_cpu_quota": info["cgroup_cpu_quota"], "affinity_cpus": info["affinity"],
+               # the CPU time the threads can actually get: min(threads, the box's cgroup quota)
+               "effective_cores": min(info["threads_all_core"], info["cgroup_cpu_quota"] or info["threads_all_core"]),
                "kind": ec["kind"] if ec else None, "sample": ec["sample"] if ec else None,
                "nproc": info["nproc"], "cpu_model": info["cpu_model"],
                "one_core": ec["one_core"] if ec else None, "all_core": ec["all_core"] if ec else None,

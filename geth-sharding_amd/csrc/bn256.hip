@@ -604,6 +604,137 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_LINES_WAV
     if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, pstat, lines, luse);
 }
 
+// ---- the lines role at TWO waves per SIMD (k_bn_lines_w2).  A configs[4] batch has 4 x 65,536 pairs:
+// 4,096 waves, two rounds of the GPU's wave slots even at two per SIMD, so unlike the Miller loop the
+// lines need no extra split to fill a second wave.  k_bn_lines holds 256 + 125 registers; what moves
+// here: P and Q wait in LDS ([54 words][64 lanes], 13.8 KB per wave) and are read where a line needs
+// them, and each line coefficient is stored to HBM as soon as it is computed instead of after the step.
+// The formulas and their order are line_double_i / line_add_i's (BN_LINES_LEAN), so the lines are the
+// same F_p^2 values.
+#define LW2_SEQ __builtin_amdgcn_sched_barrier(0)
+GSV_DI void lw2_put(uint32_t* l, int j, const fq& v) {
+#pragma unroll
+    for (int w = 0; w < 9; w++) l[(j * 9 + w) * 64] = v.v[w];
+}
+GSV_DI fq lw2_get(const uint32_t* l, int j) {
+    fq r;
+#pragma unroll
+    for (int w = 0; w < 9; w++) r.v[w] = l[(j * 9 + w) * 64];
+    return r;
+}
+// the lane's LDS column: P.x, P.y, Q.x.x, Q.x.y, Q.y.x, Q.y.y
+GSV_DI g2a lw2_q(const uint32_t* l) { return g2a{fp2{lw2_get(l, 2), lw2_get(l, 3)}, fp2{lw2_get(l, 4), lw2_get(l, 5)}}; }
+// optate.go:52-92 (line_double_i, LEAN order), l.a / l.b / l.c stored as computed
+GSV_DI void line_double_w2(g2j& r, const uint32_t* l, uint32_t* __restrict__ lines, uint32_t n, uint32_t j, int li) {
+    const fp2 A = s2(fp2_sqr(r.x));
+    const fp2 B = s2(fp2_sqr(r.y));
+    const fp2 C = s2(fp2_sqr(B));
+    const fp2 D = s2(fp2_dbl(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.x, B)), A), C)));
+    const fp2 E = s2(fp2_add(fp2_dbl(A), A));
+    const fp2 G = s2(fp2_sqr(E));
+    LW2_SEQ;
+    soa_store2(lines, n, j, li * 6 + 0, s2(fp2_sub(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.x, E)), A), G), fp2_mul_small<4>(B))));
+    LW2_SEQ;
+    const fp2 oz = s2(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.y, r.z)), B), r.t));
+    LW2_SEQ;
+    soa_store2(lines, n, j, li * 6 + 2, s2(fp2_mul_fp(fp2_neg(fp2_dbl(fp2_mul(E, r.t))), lw2_get(l, 0))));
+    LW2_SEQ;
+    soa_store2(lines, n, j, li * 6 + 4, s2(fp2_mul_fp(fp2_dbl(fp2_mul(oz, r.t)), lw2_get(l, 1))));
+    LW2_SEQ;
+    r.x = s2(fp2_sub(G, fp2_dbl(D)));
+    r.y = s2(fp2_sub(fp2_mul(fp2_sub(D, r.x), E), fp2_mul_small<8>(C)));
+    r.z = oz;
+    r.t = s2(fp2_sqr(oz));
+}
+// optate.go:3-50 (line_add_i: r + p, p affine, r2 = p.y^2), ordered to end each value's life early
+GSV_DI void line_add_w2(g2j& r, const g2a& p, const fp2& r2, const uint32_t* l, uint32_t* __restrict__ lines, uint32_t n,
+                        uint32_t j, int li) {
+    const fp2 H = s2(fp2_sub(fp2_mul(p.x, r.t), r.x));  // B - r.x
+    const fp2 L1 = s2(fp2_sub(fp2_mul(fp2_sub(fp2_sub(fp2_sqr(fp2_add(p.y, r.z)), r2), r.t), r.t), fp2_dbl(r.y)));  // D - 2 r.y
+    LW2_SEQ;
+    const fp2 I = s2(fp2_sqr(H));
+    const fp2 E = s2(fp2_mul_small<4>(I));
+    const fp2 J = s2(fp2_mul(H, E));
+    const fp2 V = s2(fp2_mul(r.x, E));
+    LW2_SEQ;
+    g2j o;
+    o.z = s2(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.z, H)), r.t), I));
+    o.x = s2(fp2_sub(fp2_sub(fp2_sqr(L1), J), fp2_dbl(V)));
+    o.y = s2(fp2_sub(fp2_mul(fp2_sub(V, o.x), L1), fp2_dbl(fp2_mul(r.y, J))));
+    o.t = s2(fp2_sqr(o.z));
+    LW2_SEQ;
+    soa_store2(lines, n, j, li * 6 + 0, s2(fp2_sub(fp2_dbl(fp2_mul(L1, p.x)), fp2_sub(fp2_sub(fp2_sqr(fp2_add(p.y, o.z)), r2), o.t))));
+    LW2_SEQ;
+    soa_store2(lines, n, j, li * 6 + 2, s2(fp2_mul_fp(fp2_dbl(fp2_neg(L1)), lw2_get(l, 0))));
+    LW2_SEQ;
+    soa_store2(lines, n, j, li * 6 + 4, s2(fp2_mul_fp(fp2_dbl(o.z), lw2_get(l, 1))));
+    r = o;
+}
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_bn_lines_w2(const uint8_t* __restrict__ in,
+                                                   const uint64_t* __restrict__ pair_src,
+                                                   uint32_t npairs, uint32_t* __restrict__ lines,
+                                                   uint8_t* __restrict__ luse, uint8_t* __restrict__ pstat) {
+    __shared__ uint32_t lds[54 * 64];
+    uint32_t* l = lds + threadIdx.x;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    (void)luse;
+    bool ok, inf1, inf2;
+    {
+        const uint8_t* s = in + pair_src[i];
+        g1a P;
+        g2a Q;
+        ok = fp_unmarshal(P.x, s);
+        ok = fp_unmarshal(P.y, s + 32) && ok;
+        ok = fp_unmarshal(Q.x.x, s + 64) && ok;  // imaginary part first (bn256.go:267-278)
+        ok = fp_unmarshal(Q.x.y, s + 96) && ok;
+        ok = fp_unmarshal(Q.y.x, s + 128) && ok;
+        ok = fp_unmarshal(Q.y.y, s + 160) && ok;
+        inf1 = fq_is_zero(P.x) && fq_is_zero(P.y);
+        inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
+        if (ok && !inf1)  // curve.go:39-52: y^2 == x^3 + 3
+            ok = fq_eq(fq_mul(P.y, P.y), fq_add(fq_mul(fq_mul(P.x, P.x), P.x), fq_const(FQ_THREE)));
+        if (ok && !inf2) ok = g2_on_twist(Q);
+        lw2_put(l, 0, P.x), lw2_put(l, 1, P.y), lw2_put(l, 2, Q.x.x), lw2_put(l, 3, Q.x.y), lw2_put(l, 4, Q.y.x),
+            lw2_put(l, 5, Q.y.y);
+    }
+    LW2_SEQ;
+    g2a Q = lw2_q(l);
+    g2j r{Q.x, Q.y, fp2_one(), fp2_one()};
+    int li = 0;
+#pragma unroll 1
+    for (int k = 64; k > 0; k--) {
+        line_double_w2(r, l, lines, npairs, i, li++);
+        const uint64_t bit = 1ull << (k - 1);
+        if ((NAF_POS | NAF_NEG) & bit) {
+            LW2_SEQ;
+            Q = lw2_q(l);
+            const fp2 r2 = s2(fp2_sqr(Q.y));
+            if (!(NAF_POS & bit)) Q.y = s2(fp2_neg(Q.y));
+            line_add_w2(r, Q, r2, l, lines, npairs, i, li++);
+        }
+        LW2_SEQ;
+    }
+    // Q1 = pi(Q), -Q2 = -pi^2(Q) (optate.go:168-209)
+    Q = lw2_q(l);
+    {
+        g2a q1{s2(fp2_mul(fp2_conj(Q.x), fp2_const(FQ_XI_P1_3_X, FQ_XI_P1_3_Y))),
+               s2(fp2_mul(fp2_conj(Q.y), fp2_const(FQ_XI_P1_2_X, FQ_XI_P1_2_Y)))};
+        line_add_w2(r, q1, s2(fp2_sqr(q1.y)), l, lines, npairs, i, li++);
+    }
+    LW2_SEQ;
+    Q = lw2_q(l);
+    {
+        g2a mq2{s2(fp2_mul_fp(Q.x, fq_const(FQ_XI_PSQ1_3))), Q.y};
+        line_add_w2(r, mq2, s2(fp2_sqr(mq2.y)), l, lines, npairs, i, li);
+    }
+    LW2_SEQ;
+    Q = lw2_q(l);
+    if (ok && !inf2) ok = g2_frob_check(r, Q);
+    pstat[i] = !ok ? PS_BAD : (inf1 || inf2) ? PS_SKIP : PS_OK;
+}
+#undef LW2_SEQ
+
 // ---- per-check multi-Miller loop.  The product of a check's Miller values equals one loop that
 // squares the shared accumulator once per step and multiplies in every pair's lines
 // (prod f_i^2 l_i = (prod f_i)^2 prod l_i, exact in F_p^12), so a check of k pairs spends one
@@ -953,8 +1084,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_MILLER_WA
 
 // ---------------------------------------------------------------- final exponentiation (optate.go:212-261)
 // The final exponentiation runs as a PROGRAM of F_p^12 operations on two values: X (the accumulator,
-// in registers) and A (the operand, in LDS: one F_p^12 per lane, 27 KB per 64-lane workgroup, so four
-// workgroups still fit a CU).  One loop executes it; its body holds a single copy of each operation,
+// in registers) and A (the operand, in LDS: one F_p^12 per lane; with a product's packed v0 beside it,
+// 156 words per lane = 39,936 B per 64-lane workgroup, so CDNA4's 160 KB of LDS per CU holds four
+// workgroups — more than the one wave per SIMD the kernel's registers allow).  One loop executes it; its body holds a single copy of each operation,
 // so k_bn_final's code stays small, and nothing is called: no call frames, no callee-saved register
 // spills, no private segment.  A product streams A's halves from LDS, so its working set is X plus
 // one F_p^6 product's (a dense F_p^6 product alone needs ~240 VGPRs of operands and column
@@ -1568,7 +1700,10 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
     const uint8_t* d_use = cc ? conc->d_luse : d_pstat;
     if (BN_SUB_FROB && npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        if (layout & GSV_BN_LAYOUT_CONC)
+        if ((layout & GSV_BN_LAYOUT_CONC) && (layout & GSV_BN_LAYOUT_LINESW2))
+            hipLaunchKernelGGL(bn::k_bn_lines_w2, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
+                               d_lines, (uint8_t*)nullptr, d_pstat);
+        else if (layout & GSV_BN_LAYOUT_CONC)
             hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
                                d_lines, (uint8_t*)nullptr, d_pstat);
         else

@@ -846,6 +846,17 @@ bool bn_miller_w2() {
     if (const char* e = getenv("GSV_BN_MILLER_W2")) return atoi(e) != 0;
     return false;
 }
+// The lines at two waves per SIMD (k_bn_lines_w2: P and Q in LDS, coefficients stored as computed; 256
+// registers, no scratch) or at one (k_bn_lines, 256 + 125).  Measured (r05, profiles/r05/ab/lines_w2_*,
+// pipe_l*): alone at 65,536 checks 5.95 vs 6.67 ms; in the two-deep pipeline equal (19.98 vs 19.96 ms per
+// batch), three deep 19.9-20.0 vs 20.2 ms; at 8,192 checks three deep 4.12 vs 3.75 ms per batch (slower:
+// its 512 waves then share SIMDs with the other batches' one-wave Miller / final waves, which a two-wave
+// budget cannot join).  So the two-wave kernel is taken from four waves' worth of pairs per SIMD up.
+// GSV_BN_LINES_W2 = 0/1 forces the choice.
+bool bn_lines_w2(size_t npairs, int cus) {
+    if (const char* e = getenv("GSV_BN_LINES_W2")) return atoi(e) != 0;
+    return npairs >= (size_t)std::max(cus, 1) * 4 * 64 * 4;
+}
 // Pairs per Miller lane.  Every lane of a check runs the 64-step loop (its F_p^12 squarings are per
 // lane), so k = 4 pairs per lane spends the fewest products; but one lane is a long dependent chain,
 // and a batch that gives the GPU's SIMDs fewer than `waves` waves each is latency-bound, so smaller
@@ -876,8 +887,9 @@ std::vector<uint64_t> pairing_key(const uint64_t* h_off, size_t n) {
     const char* m = getenv("GSV_BN_MILLER2");
     const char* cc = getenv("GSV_BN_CONC");
     const char* w2 = getenv("GSV_BN_MILLER_W2");
+    const char* lw = getenv("GSV_BN_LINES_W2");
     std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0, m ? (uint64_t)atoi(m) + 1 : 0,
-                              cc ? (uint64_t)atoi(cc) + 1 : 0, w2 ? (uint64_t)atoi(w2) + 1 : 0};
+                              cc ? (uint64_t)atoi(cc) + 1 : 0, w2 ? (uint64_t)atoi(w2) + 1 : 0, lw ? (uint64_t)atoi(lw) + 1 : 0};
     key.insert(key.end(), h_off, h_off + n + 1);
     return key;
 }
@@ -946,7 +958,8 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.deep = depth >= 3;
     s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
                (bn_miller2(s.nl, cus, depth) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
-               (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0) | (bn_miller_w2() ? gsv::GSV_BN_LAYOUT_MILLERW2 : 0);
+               (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0) | (bn_miller_w2() ? gsv::GSV_BN_LAYOUT_MILLERW2 : 0) |
+               (bn_lines_w2(np, cus) ? gsv::GSV_BN_LAYOUT_LINESW2 : 0);
     s.o_src = L.add(np * 8 + 8);
     s.o_pidx = L.add(np * 4 + 4);
     s.o_lfirst = L.add((s.nl + 1) * 4);

@@ -20,11 +20,6 @@
 
 namespace gsv {
 
-// 1: k_notary_tx stages each wave's chunk span in LDS before decoding (0: global byte loads, A/B)
-#ifndef GSV_NOTARY_STAGE
-#define GSV_NOTARY_STAGE 1
-#endif
-
 struct BlobRec {
     uint32_t first_chunk;  // chunk index in the shard body
     uint32_t nchunks;
@@ -87,23 +82,14 @@ __global__ __launch_bounds__(BI_THREADS) void k_blob_index(const uint8_t* __rest
 }
 
 // ---------------------------------------------------------------- one transaction per lane
-// Data byte k of a blob sits at chunk k/31, offset 1 + k%31.  When the wave's chunk span is staged in
-// LDS (k_notary_tx), `lds` is the wave's column base and `loff` the blob's first chunk in the span: the
-// span's byte o lives at row o/256, column o%256 of the GLV table's [row][256 lanes x 4 B] layout (the
-// wave's own 256-byte column of each 1-KB row, so no other wave's table writes can reach it).
-typedef __attribute__((address_space(3))) const uint8_t lds_u8;  // an LDS byte (ds_read_u8, not a flat load)
+// Measured and not kept (r05): staging each wave's chunk span in its columns of the GLV table's LDS rows
+// (free until recover_core builds the table) and decoding from LDS instead of single-byte global loads:
+// tx kernels 8.45-8.66 vs 8.60-8.67 ms per configs[3] step (profiles/r05/ab/recover_ab_*.json), within
+// noise.  The per-tx gap to k_ecrecover is the chunk roots the notary runs beside the tx kernel on its
+// side stream (~1 ms of every 8.5 ms step shares the SIMDs), not the decode.
 struct BlobView {
-    const uint8_t* base;  // first chunk of the blob (global)
-    lds_u8* lds = nullptr;
-    uint32_t loff = 0;
-    GSV_DI uint8_t at(uint32_t k) const {
-        const uint32_t pos = (k / 31) * 32 + 1 + k % 31;
-        if (lds) {  // wave-uniform
-            const uint32_t o = loff + pos;
-            return lds[(o >> 8) * 1024 + (o & 255)];
-        }
-        return base[pos];
-    }
+    const uint8_t* base;  // first chunk of the blob
+    GSV_DI uint8_t at(uint32_t k) const { return base[(size_t)(k / 31) * 32 + 1 + k % 31]; }
 };
 
 struct RItem {
@@ -272,46 +258,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
         if ((lane & 7u) == 0 && t < max_txs && (t >> 3) < bm_bytes) bitmap[(size_t)shard * bm_bytes + (t >> 3)] = 0;
         return;
     }
-    // Stage the chunk span of the wave's transactions (consecutive blobs: one contiguous range of the
-    // body) in the wave's columns of the GLV table's LDS rows, which are free until recover_core
-    // builds the table: the decode below then reads its bytes from LDS instead of issuing ~300
-    // single-byte global loads per transaction, each wave-instruction touching 64 cache lines
-    // (r05; the r04 kernel ran 10.5 ns per tx against k_ecrecover's 8.7).  A span too long for the
-    // 18 KB of columns is read from HBM as before.
-    const uint8_t* body = bodies + body_off[shard];
-    lds_u8* wlds = nullptr;
-    uint32_t c_lo = 0, a16 = 0;
-#if GSV_NOTARY_STAGE && GSV_GLV_TAB != 1
-    {
-        constexpr uint32_t CAP = 18u * GLV_LNT * 256u;  // bytes of the wave's columns
-        const uint32_t t0 = t - lane, nw = min(64u, n - t0);  // n > t0: the wave has an active lane
-        const BlobRec r0 = blobs[(size_t)shard * max_txs + t0], r1 = blobs[(size_t)shard * max_txs + t0 + nw - 1];
-        c_lo = r0.first_chunk;
-        const uint8_t* g = body + (size_t)c_lo * 32;
-        a16 = (uint32_t)((uintptr_t)g & 15u);
-        const uint32_t span = (r1.first_chunk + r1.nchunks - c_lo) * 32 + a16;  // bytes from g - a16
-        if (span + 16 <= CAP) {  // wave-uniform
-            // a 16-byte aligned piece holding a body byte never crosses a page
-            const uint4* src = (const uint4*)(g - a16);
-            uint8_t* col = (uint8_t*)ltab + (threadIdx.x & ~63u) * 4u;
-            const uint32_t nv = (span + 15) >> 4;
-            for (uint32_t v = lane; v < nv; v += 64) {
-                const uint32_t o = v << 4;
-                *(uint4*)(col + (o >> 8) * 1024 + (o & 255)) = src[v];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            wlds = (lds_u8*)col;
-        }
-    }
-#endif
     uint32_t st = GSV_ST_BAD_RLP;
     uint32_t msg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, r[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t vbyte = 0, vbig = 1, homestead = 1;
     if (active) {
         BlobRec br = blobs[(size_t)shard * max_txs + t];
-        BlobView b{body + (size_t)br.first_chunk * 32, wlds, a16 + (br.first_chunk - c_lo) * 32};
+        BlobView b{bodies + body_off[shard] + (size_t)br.first_chunk * 32};
         RItem outer, f[9];
         uint32_t used = rlp_item(b, 0, br.len, outer);
         bool ok = used && used == br.len && outer.list;

@@ -70,7 +70,11 @@ def _random_inputs(oracle, seed):
     return inputs
 
 
-def test_pairing_random_batch_vs_oracle(ctx, oracle):
+@pytest.mark.parametrize("lines_w2", ["0", "1"])
+def test_pairing_random_batch_vs_oracle(ctx, oracle, monkeypatch, lines_w2):
+    """Both lines kernels (k_bn_lines_w2, the default: two waves per SIMD with P, Q in LDS; k_bn_lines:
+    one wave) give the oracle's verdicts on valid, false, malformed, infinite and ragged checks."""
+    monkeypatch.setenv("GSV_BN_LINES_W2", lines_w2)
     inputs = _random_inputs(oracle, 17)
     out = ctx.pairing_check_batch(inputs)
     want = np.array([_v(oracle, x) for x in inputs], np.uint8)
@@ -115,7 +119,7 @@ def test_pairing_two_wave_miller(ctx, oracle, monkeypatch, k):
     assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
 
 
-@pytest.mark.parametrize("layout", ["auto", "k1", "k2", "k4", "final3", "final1", "miller2", "w2"])
+@pytest.mark.parametrize("layout", ["auto", "k1", "k2", "k4", "final3", "final1", "miller2", "w2", "lines1"])
 def test_configs4_rank_batch_depth_three(ctx, monkeypatch, layout):
     """The N = 8 per-rank share of configs[4]: 8,192 checks from the configs[4] generator (seed 5000, all
     six seeded classes: G1 / G2 infinity pairs, (inf, outside-G2 Q), (inf, off-twist Q), a pair with Q
@@ -125,7 +129,8 @@ def test_configs4_rank_batch_depth_three(ctx, monkeypatch, layout):
     import torch
     env = {"k1": ("GSV_BN_PAIRS_PER_LANE", "1"), "k2": ("GSV_BN_PAIRS_PER_LANE", "2"),
            "k4": ("GSV_BN_PAIRS_PER_LANE", "4"), "final3": ("GSV_BN_FINAL3", "1"),
-           "final1": ("GSV_BN_FINAL3", "0"), "miller2": ("GSV_BN_MILLER2", "1"), "w2": ("GSV_BN_MILLER_W2", "1")}
+           "final1": ("GSV_BN_FINAL3", "0"), "miller2": ("GSV_BN_MILLER2", "1"), "w2": ("GSV_BN_MILLER_W2", "1"),
+           "lines1": ("GSV_BN_LINES_W2", "0")}
     if layout in env:
         monkeypatch.setenv(*env[layout])
     n = 8192

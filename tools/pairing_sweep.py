@@ -98,9 +98,26 @@ def run_pipelined(ctx, n, depth, steps=12):
     return (time.perf_counter() - t0) / steps
 
 
+def preheat(ctx, seconds=1.5):
+    """GPU-busy for a while before anything is timed (SWEEP_PREHEAT=1): the first pipelined run of a
+    process read ~1.5x slow even after its own warm-up batches (profiles/r05/ab/pipe_rep_8192.txt)."""
+    n = 65536
+    pin = torch.empty((n, 768), dtype=torch.uint8, device="cuda")
+    ctx.bn256_synth_checks_dev(5000, pin, None)
+    torch.cuda.synchronize()
+    off = np.arange(n + 1, dtype=np.uint64) * 768
+    pv = torch.empty((n,), dtype=torch.uint8, device="cuda")
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        ctx.pairing_check_batch_dev(pin, off, pv)
+        torch.cuda.synchronize()
+
+
 def main():
     sizes = [int(a) for a in sys.argv[1:]] or [65536, 32768, 16384, 8192]
     ctx = gsv.default_context()
+    if os.environ.get("SWEEP_PREHEAT"):
+        preheat(ctx)
     if os.environ.get("SWEEP_PIPELINE"):  # e.g. "1,2,3": pipeline depths at auto layout
         for n in sizes:
             for d in (int(x) for x in os.environ["SWEEP_PIPELINE"].split(",")):

@@ -28,7 +28,10 @@ def main(root):
             with open(os.path.join(root, "trace_logs", f"bench_under_trace_{leg}.json")) as f:
                 bench_ms = get(json.loads(f.read()))
             with open(os.path.join(root, f"kernel_stats_{leg}.csv")) as f:
-                rows = [r for r in csv.DictReader(f) if r["Name"].startswith(kname + "(")]
+                allrows = list(csv.DictReader(f))
+            # the pairing's lines kernel runs as k_bn_lines_w2 at large batches (r05): either name
+            rows = [r for r in allrows if r["Name"].startswith(kname + "(")] or \
+                [r for r in allrows if r["Name"].startswith(kname + "_w2(")]
         except (OSError, KeyError, ValueError):
             continue
         if not rows:
