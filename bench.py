@@ -793,10 +793,10 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     # consecutive batches on `depth` streams with their own shape instances (as the chunk-root leg):
     # one batch's latency-bound Miller / final-exponentiation waves share the SIMDs with the next
     # batch's kernels
-    # auto: three batches in flight for the per-rank batch of N > 1 (the layout then turns work-efficient,
-    # 8,192 checks 4.67 -> 3.73 ms per batch), two at 65,536 (3 % slower at three;
-    # profiles/r03/ab_pairing_depth.txt)
-    depth = args.pairing_pipeline if args.pairing_pipeline > 0 else (3 if nloc < 65536 else 2)
+    # auto: four batches in flight for the per-rank batch of N > 1 (the layout then turns work-efficient:
+    # 8,192 checks 4.5 ms per batch at depth 2, 3.75 at 3, 3.62-3.65 at 4; profiles/r05/ab/pipe_l0_m0_8192.txt),
+    # two at 65,536 (1 % slower at three; profiles/r03/ab_pairing_depth.txt, r05/ab/pipe_l1_m0_65536.txt)
+    depth = args.pairing_pipeline if args.pairing_pipeline > 0 else (4 if nloc < 65536 else 2)
     ctx.set_pipeline_depth(depth)
     streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
     pvk = [pver] + [torch.empty_like(pver) for _ in range(depth - 1)]
@@ -968,7 +968,7 @@ def main():
                     help="streams (shape instances) consecutive chunk-root batches are spread over")
     ap.add_argument("--pairing-pipeline", type=int, default=0,
                     help="streams (shape instances) consecutive pairing batches are spread over "
-                         "(0 = auto: 3 below 65,536 checks per rank, else 2)")
+                         "(0 = auto: 4 below 65,536 checks per rank, else 2)")
     ap.add_argument("--notary-pipeline", type=int, default=2,
                     help="streams (shape instances) consecutive notary partition steps are spread over")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rank plumbing only (no GPU)")

@@ -49,7 +49,8 @@
  *     for the *_dev calls; host-pointer calls serialize on the context's internal stream.
  *   - stream = NULL selects the context stream, a blocking stream: it is ordered both ways with work
  *     on the process's legacy default (NULL) stream, such as PyTorch's default stream.  Work on other
- *     non-blocking streams is the caller's to order (events), as for any stream argument.
+ *     non-blocking streams is the caller's to order (events), as for any stream argument.  Capture
+ *     HIP graphs on an explicit stream (a NULL-stream capture would join that implicit ordering).
  */
 #ifndef GSV_H
 #define GSV_H
