@@ -79,7 +79,7 @@ VALU_ISSUE_PEAK = 0.5
 PEAK_LANE_OPS = SIMDS * 64 * VALU_ISSUE_PEAK * CLOCK          # 7.86e13 full-rate 32-bit lane-ops/s
 PEAK_MAC = SIMDS * 16 * CLOCK                                 # 3.93e13 v_mad_u64_u32 lane-ops/s
 HBM_PEAK_GBPS = 8000.0
-ROUND = "r04"
+ROUND = "r05"
 PROFILES = os.path.join(ROOT, "profiles", ROUND)
 LEGS = ["ecrecover", "chunk_root", "notary", "keccak", "tx_root", "poc", "headers", "pairing"]
 
@@ -425,7 +425,9 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
     # batch's leaf level, as a notary validating a stream of collations would run them
     depth = max(1, args.pipeline)
     ctx.set_pipeline_depth(depth)
-    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
+    # the pipeline's streams on hardware queues of their own (gsv_stream_create): torch's pool streams
+    # can share one of HIP's four in-order queues, and batches on them then serialise
+    streams = pipeline_streams(ctx, depth, stream, dev)
     rootk = [torch.empty((N_SHARDS, 32), dtype=torch.uint8, device=dev) for _ in range(depth)]
     roots = rootk[0]
     ctx.chunk_root_prepare(h_off)
@@ -447,6 +449,7 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
         s_.synchronize()
     barrier(ws)
     cdt = max_over_ranks(time.perf_counter() - t1, ws)
+    ctx.destroy_streams(streams)
     # per-kernel breakdown from a separate, instrumented pass
     ctx.reset_timing()
     ctx.set_timing(True)
@@ -539,11 +542,12 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     ctx.set_pipeline_depth(depth)
     ctx.notary_partition_prepare(n_off, N_SHARDS, ws, rank, max_txs=NOTARY_TXS)
     ctx.set_pipeline_depth(1)
-    n_streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
+    n_streams = pipeline_streams(ctx, depth, stream, dev)  # on queues of their own (as the chunk-root leg)
     outs = [(a_root, a_ntx, a_bm, a_rst)] + [(torch.zeros_like(a_root), torch.zeros_like(a_ntx), torch.zeros_like(a_bm),
                                              torch.full_like(a_rst, -1)) for _ in range(depth - 1)]
-    for s_ in n_streams[1:]:
+    for s_ in n_streams:
         s_.wait_stream(torch.cuda.current_stream())
+        s_.wait_stream(stream)
 
     def notary_step(with_status=False, i=0):
         r_, c_, b_, st_ = outs[i % depth]
@@ -552,7 +556,7 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
                                           stream=n_streams[i % depth], prepare=False)
 
     notary_step(with_status=True)
-    stream.synchronize()
+    n_streams[0].synchronize()
     # full-size parity: every tx status of this rank's block equals the construction, and the gathered
     # records of all 100 shards equal the committed configs[3] fixture (oracle/_ref + restatement)
     assert int(a_rst.min()) == 0 and int(a_rst.max()) == 0, f"rank statuses {a_rst.tolist()}"
@@ -603,8 +607,9 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     ctx.reset_timing()  # kernel breakdown from a separate, instrumented step
     ctx.set_timing(True)
     notary_step()
-    stream.synchronize()
+    n_streams[0].synchronize()
     ctx.set_timing(False)
+    ctx.destroy_streams(n_streams)
     k_not, _ = ctx.kernel_time(_lib.K_NOTARY)
     assert int(a_rst.max()) == 0
     out = {"shards_per_s": round(N_SHARDS * nsteps / ndt, 2),
@@ -779,10 +784,22 @@ def leg_headers(ctx, stream, dev, ws, rank, args, sig):
     return {"headers_per_s": round(ws * nh * hsteps / hdt, 1), "headers": nh, "ms_per_step": round(hdt / hsteps * 1e3, 3)}
 
 
+def pipeline_streams(ctx, depth, stream, dev):
+    """The streams a leg's pipeline spreads consecutive batches over: on hardware queues of their own
+    (gsv_stream_create); GSV_BENCH_TORCH_STREAMS=1 takes the leg's stream and torch pool streams instead
+    (A/B: those can share one of HIP's four in-order queues)."""
+    import torch
+    if os.environ.get("GSV_BENCH_TORCH_STREAMS") == "1":
+        return [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
+    return ctx.pipeline_streams(depth)
+
+
 def leg_pairing(ctx, stream, dev, ws, rank, args):
     import torch
     from gsv import _lib
     nloc = N_CHECKS // ws + (1 if rank < N_CHECKS % ws else 0)
+    if args.pairing_checks:  # one GPU standing in for a rank of an N-GPU run (8,192 = N = 8)
+        nloc = args.pairing_checks
     pin = torch.empty((nloc, 768), dtype=torch.uint8, device=dev)
     pexp = torch.empty((nloc,), dtype=torch.uint8, device=dev)
     pver = torch.empty((nloc,), dtype=torch.uint8, device=dev)
@@ -792,13 +809,13 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     stream.synchronize()
     # consecutive batches on `depth` streams with their own shape instances (as the chunk-root leg):
     # one batch's latency-bound Miller / final-exponentiation waves share the SIMDs with the next
-    # batch's kernels
-    # auto: four batches in flight for the per-rank batch of N > 1 (the layout then turns work-efficient:
-    # 8,192 checks 4.5 ms per batch at depth 2, 3.75 at 3, 3.62-3.65 at 4; profiles/r05/ab/pipe_l0_m0_8192.txt),
-    # two at 65,536 (1 % slower at three; profiles/r03/ab_pairing_depth.txt, r05/ab/pipe_l1_m0_65536.txt)
-    depth = args.pairing_pipeline if args.pairing_pipeline > 0 else (4 if nloc < 65536 else 2)
+    # batch's kernels.  auto (r05, streams on queues of their own, profiles/r05/ab/pairing_depth_dedicated.txt):
+    # four batches in flight below 65,536 checks (8,192: 6.47 / 4.53 / 3.76 / 3.67 ms per batch at depth
+    # 1-4; 16,384: 7.72 / 6.98 / 6.26 / 6.23), one at 65,536 and up, where every kernel alone fills the
+    # GPU and overlapping batches only contend (19.56 / 20.57 / 20.56 / 20.20 ms)
+    depth = args.pairing_pipeline if args.pairing_pipeline > 0 else (4 if nloc < 65536 else 1)
     ctx.set_pipeline_depth(depth)
-    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
+    streams = pipeline_streams(ctx, depth, stream, dev)  # on queues of their own (as the chunk-root leg)
     pvk = [pver] + [torch.empty_like(pver) for _ in range(depth - 1)]
     ctx.pairing_prepare(p_off)
     ctx.set_pipeline_depth(1)
@@ -808,7 +825,9 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
         s_.synchronize()
     # size-independent parity property at full size: every verdict equals the generator's
     assert all(torch.equal(v, pexp) for v in pvk), "pairing verdicts differ from the constructed truth"
-    psteps = 6 if depth <= 3 else 2 * depth
+    # small per-rank batches: enough batches that the pipeline's fill and drain (about one batch
+    # latency, depth x the per-batch time) stay a small part of the timed region
+    psteps = (6 if depth <= 3 else 2 * depth) if nloc >= 65536 else 6 * depth
     barrier(ws)
     t2 = time.perf_counter()
     for i in range(psteps):
@@ -817,6 +836,7 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
         s_.synchronize()
     barrier(ws)
     pdt = max_over_ranks(time.perf_counter() - t2, ws)
+    ctx.destroy_streams(streams)
     assert all(torch.equal(v, pexp) for v in pvk), "pairing verdicts differ from the constructed truth"
     # per-kernel breakdown from a separate, instrumented single-stream pass
     ctx.reset_timing()
@@ -862,7 +882,8 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
                                     "kernels execute per check (9x29-bit F_p products 81 + Montgomery reductions 81; "
                                     "psi subgroup test, precomputed lines, multi-Miller loop; instrumented build, "
                                     "profiles/{ROUND}/opcount.json)".format(ROUND=ROUND)}
-    out = {"checks_per_s": round(N_CHECKS * psteps / pdt, 1), "checks": N_CHECKS, "checks_per_rank": nloc,
+    total = nloc * ws if args.pairing_checks else N_CHECKS
+    out = {"checks_per_s": round(total * psteps / pdt, 1), "checks": total, "checks_per_rank": nloc,
            "pipeline_depth": depth,
            "pairs_per_check": 4, "roofline": roof, "ms_per_step": round(pdt / psteps * 1e3, 3),
            "prepare_kernel_ms": round(k_prep / psteps, 3), "miller_kernel_ms": round(k_mill / psteps, 3),
@@ -969,8 +990,13 @@ def main():
     ap.add_argument("--pairing-pipeline", type=int, default=0,
                     help="streams (shape instances) consecutive pairing batches are spread over "
                          "(0 = auto: 4 below 65,536 checks per rank, else 2)")
-    ap.add_argument("--notary-pipeline", type=int, default=2,
-                    help="streams (shape instances) consecutive notary partition steps are spread over")
+    ap.add_argument("--pairing-checks", type=int, default=0,
+                    help="checks per rank in the pairing leg (0 = configs[4]'s 65,536 split over the ranks; "
+                         "8192 rehearses a rank of the 8-GPU run on one GPU)")
+    ap.add_argument("--notary-pipeline", type=int, default=3,
+                    help="streams (shape instances) consecutive notary partition steps are spread over "
+                         "(r05, queues of their own: 1 / 2 / 3 deep 10,560 / 11,457 / 11,623 shards/s, "
+                         "profiles/r05/ab/chunk_notary_depth.txt)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rank plumbing only (no GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -96,7 +96,7 @@ struct Shape {
     // GSV_BN_LAYOUT_CONC: per instance, the side stream and fork/join events (created at prepare)
     std::vector<hipStream_t> side;
     std::vector<hipEvent_t> efork, ejoin;
-    bool side_borrowed = false;  // host-path shape: the context's side stream and events, not its own
+    bool side_borrowed = false;  // host-path shape: the context's side events too, not its own
     // SK_NOTARY
     uint32_t max_txs = 0, sfx_len = 0;
     int signer_kind = 0;
@@ -125,9 +125,7 @@ struct Shape {
                 if (e) hipEventDestroy(e);
             for (hipEvent_t e : ejoin)
                 if (e) hipEventDestroy(e);
-            for (hipStream_t q : side)
-                if (q) hipStreamDestroy(q);
-        }
+        }  // the side streams are the context's (gsv_ctx::sides) or, host path, its hside
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : bulk_ev)
@@ -185,6 +183,10 @@ struct gsv_ctx {
     // the host paths' side stream and fork/join events (lent to their per-call shapes)
     hipStream_t hside = nullptr;
     hipEvent_t hfork = nullptr, hjoin = nullptr;
+    // the prepared shapes' side streams, per instance index, on hardware queues of their own
+    // (own_queue_stream: HIP's four shared in-order queues would order a side chain after unrelated
+    // work; the notary pipeline two deep measured 11,734 vs 11,419 shards/s, profiles/r05/ab/notary_sweep_*)
+    std::vector<hipStream_t> sides;
     int pipeline_depth = 1;  // instances per prepared shape (gsv_ctx_set_pipeline_depth)
 };
 
@@ -493,6 +495,19 @@ int chunk_run(gsv_ctx* c, const Shape& s, const ChunkLaunch& cl, const uint8_t* 
     return GSV_SUCCESS;
 }
 
+int device_cus(int device);
+
+// A stream on an HSA queue of its own: HIP multiplexes ordinary streams over GPU_MAX_HW_QUEUES (4) shared
+// in-order queues, but backs a CU-masked stream (here: every CU) by a dedicated queue.  It is ordered with
+// the legacy NULL stream like a hipStreamDefault stream.
+int own_queue_stream(int device, hipStream_t* q) {
+    const int cus = device_cus(device);
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int i = 0; i < cus; i++) mask[i / 32] |= 1u << (i % 32);
+    HIPCHK(hipExtStreamCreateWithCUMask(q, (uint32_t)mask.size(), mask.data()));
+    return GSV_SUCCESS;
+}
+
 }  // namespace
 
 extern "C" {
@@ -559,6 +574,7 @@ void gsv_ctx_destroy(gsv_ctx* c) {
     drain_timing(c);
     for (auto e : c->free_events) hipEventDestroy(e);
     c->shapes.clear();
+    for (hipStream_t q : c->sides) hipStreamDestroy(q);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->coll_ev) hipEventDestroy(c->coll_ev);
     if (c->hfork) hipEventDestroy(c->hfork);
@@ -573,6 +589,28 @@ void gsv_ctx_destroy(gsv_ctx* c) {
 int gsv_ctx_set_timing(gsv_ctx* c, int enable) {
     if (!c) return GSV_E_INVALID_ARG;
     c->timing = enable ? 1 : 0;
+    return GSV_SUCCESS;
+}
+
+// A pipeline's streams on queues of their own (gsv.h): r05 measured 8,192-check pairing batches three
+// deep at 6.0 or 3.75 ms per batch by which of torch's pool streams the caller took (two of the three on
+// one HSA queue in the kernel trace), 3.75 on every set of CU-masked streams
+// (profiles/r05/ab/stream_sets_*).
+int gsv_stream_create(gsv_ctx* c, void** stream_out) {
+    if (!c || !stream_out) return GSV_E_INVALID_ARG;
+    *stream_out = nullptr;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t q = nullptr;
+    int rc = own_queue_stream(c->device, &q);
+    if (rc) return rc;
+    *stream_out = (void*)q;
+    return GSV_SUCCESS;
+}
+
+int gsv_stream_destroy(gsv_ctx* c, void* stream) {
+    if (!c || !stream) return GSV_E_INVALID_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamDestroy((hipStream_t)stream));
     return GSV_SUCCESS;
 }
 
@@ -986,13 +1024,21 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
 }
 // a side stream and fork/join events per instance (at prepare / host-path build), for shapes that run
 // two independent launch chains at once: the pairing's concurrent layout, the notary's chunk roots
-int shape_side_init(Shape& s) {
+int shape_side_init(gsv_ctx* c, Shape& s) {
     if (!s.side.empty()) return GSV_SUCCESS;
     s.side.assign(s.ninst, nullptr);
     s.efork.assign(s.ninst, nullptr);
     s.ejoin.assign(s.ninst, nullptr);
     for (int k = 0; k < s.ninst; k++) {
-        HIPCHK(hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking));
+        // instance k's side stream: the context's k-th, on a hardware queue of its own (shared by the
+        // shapes: only their side chains on one instance index are ordered after each other)
+        while ((int)c->sides.size() <= k) {
+            hipStream_t q = nullptr;
+            int rc = own_queue_stream(c->device, &q);
+            if (rc) return rc;
+            c->sides.push_back(q);
+        }
+        s.side[k] = c->sides[k];
         HIPCHK(hipEventCreateWithFlags(&s.efork[k], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&s.ejoin[k], hipEventDisableTiming));
     }
@@ -1015,7 +1061,7 @@ int shape_side_borrow(gsv_ctx* c, Shape& s) {
 // the concurrent layout forks onto a side stream only in the BN_SUB_FROB = 0 build (check waves)
 int pairing_conc_init(gsv_ctx* c, Shape& s, bool host_path) {
     if (!(s.layout & gsv::GSV_BN_LAYOUT_CONC) || !gsv::bn256_layout_forks()) return GSV_SUCCESS;
-    return host_path ? shape_side_borrow(c, s) : shape_side_init(s);
+    return host_path ? shape_side_borrow(c, s) : shape_side_init(c, s);
 }
 int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verdict, hipStream_t st) {
     gsv::BnConcurrent conc{};
@@ -1621,7 +1667,7 @@ int gsv_notary_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n_shards, const
                    },
                    &s);
     if (rc) return rc;
-    return shape_side_init(*s);
+    return shape_side_init(c, *s);
 }
 
 int gsv_notary_validate_shards_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n_shards,
@@ -1763,7 +1809,7 @@ int gsv_notary_partition_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n_tot
                    },
                    &s);
     if (rc) return rc;
-    return d.n ? shape_side_init(*s) : GSV_SUCCESS;
+    return d.n ? shape_side_init(c, *s) : GSV_SUCCESS;
 }
 
 int gsv_notary_partition_pack_dev(gsv_ctx* c, const uint8_t* d_bodies, const uint64_t* h_off, size_t n_total,

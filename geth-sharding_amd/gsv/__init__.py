@@ -55,10 +55,14 @@ class Context:
         check(L.gsv_ctx_create(int(device), ctypes.byref(h)))
         self._h = h
         self.device = int(device)
+        self._streams = []  # gsv_stream_create handles not yet destroyed
 
     # -------------------------------------------------------------- lifecycle / timing
     def close(self):
         if getattr(self, "_h", None):
+            for q in self._streams:
+                _lib.load().gsv_stream_destroy(self._h, q)
+            self._streams = []
             _lib.load().gsv_ctx_destroy(self._h)
             self._h = None
 
@@ -85,6 +89,27 @@ class Context:
         """Instances per prepared shape from now on (gsv_ctx_set_pipeline_depth): *_dev calls of one
         shape on up to `depth` streams run concurrently."""
         check(_lib.load().gsv_ctx_set_pipeline_depth(self._h, int(depth)))
+
+    def pipeline_streams(self, n: int):
+        """`n` streams on hardware queues of their own (gsv_stream_create), as torch ExternalStreams: the
+        streams of a pipeline of `n` batches (torch's pool streams can share an in-order queue, and
+        batches on them then serialise)."""
+        import torch
+        out = []
+        for _ in range(int(n)):
+            q = ctypes.c_void_p()
+            check(_lib.load().gsv_stream_create(self._h, ctypes.byref(q)))
+            self._streams.append(q.value)
+            out.append(torch.cuda.ExternalStream(q.value, device=torch.device("cuda", self.device)))
+        return out
+
+    def destroy_streams(self, streams):
+        """Destroys streams from pipeline_streams (after their work)."""
+        for st in streams:
+            q = int(st.cuda_stream)
+            if q in self._streams:
+                self._streams.remove(q)
+                check(_lib.load().gsv_stream_destroy(self._h, q))
 
     def reset_timing(self):
         check(_lib.load().gsv_ctx_reset_timing(self._h))

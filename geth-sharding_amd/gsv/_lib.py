@@ -100,6 +100,8 @@ SIGNATURES = [
                                                              _vp]),
     ("gsv_ctx_prepared_shapes", ctypes.c_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
     ("gsv_ctx_set_pipeline_depth", ctypes.c_int, [_vp, ctypes.c_int]),
+    ("gsv_stream_create", ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    ("gsv_stream_destroy", ctypes.c_int, [_vp, _vp]),
     ("gsv_ecrecover_precompile_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("gsv_ecrecover_precompile_batch_dev", ctypes.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
     ("gsv_chunk_root_prepare", ctypes.c_int, [_vp, _vp, _sz]),

@@ -140,6 +140,15 @@ int gsv_ctx_prepared_shapes(gsv_ctx *ctx, size_t *count, size_t *device_bytes);
  * latency-bound tail (trie top, final exponentiation) with the next batch's bulk kernels. */
 #define GSV_MAX_PIPELINE_DEPTH 8
 int gsv_ctx_set_pipeline_depth(gsv_ctx *ctx, int depth);
+/* A stream for a pipelining caller, on a hardware (HSA) queue of its own.  HIP multiplexes ordinary
+ * streams over GPU_MAX_HW_QUEUES (4) in-order queues, so two of a caller's streams can share one, and
+ * batches issued on them then run one after the other (including every event wait placed on them): a
+ * pipeline of D batches needs D streams on D queues.  The stream is created with a CU mask of every CU
+ * of the context's device (hipExtStreamCreateWithCUMask: HIP backs such a stream by a dedicated queue);
+ * it is ordered with the legacy NULL stream like a hipStreamDefault stream.  Destroy it with
+ * gsv_stream_destroy (after its work) before the context. */
+int gsv_stream_create(gsv_ctx *ctx, void **stream_out);
+int gsv_stream_destroy(gsv_ctx *ctx, void *stream);
 
 /* ---- Keccak-256 (A10) ----
  * Message i is data[off[i] .. off[i+1]); out32[32*i .. +32) = Keccak256(message i). */

@@ -54,3 +54,12 @@ def test_shard_range_matches_partition_arithmetic():
                     for r in range(world)]
             assert got == want
             assert sum(c for _, c in got) == n
+
+
+def test_stream_entry_points_reject_null_arguments():
+    """gsv_stream_create / gsv_stream_destroy check their arguments before any HIP call (no GPU needed)"""
+    from gsv import _lib
+    L = _lib.load()
+    q = ctypes.c_void_p()
+    assert L.gsv_stream_create(None, ctypes.byref(q)) == _lib.E_INVALID_ARG
+    assert L.gsv_stream_destroy(None, None) == _lib.E_INVALID_ARG

@@ -165,3 +165,35 @@ def test_generator_then_default_stream_check(ctx):
     same_in = torch.equal(pin, ref_in)  # default stream, no sync
     same_exp = torch.equal(exp, ref_exp)
     assert same_in and same_exp
+
+
+def test_pipeline_streams_on_queues_of_their_own(ctx):
+    """gsv_stream_create: a pipeline of batches over dedicated-queue streams gives the generator's
+    verdicts on every instance, orders after default-stream work (the streams are blocking), and the
+    streams are destroyed cleanly; ordering and results only (the timing A/B is
+    profiles/r05/ab/stream_sets_*)"""
+    import torch
+    _null_stream()
+    n, depth = 2048, 3
+    pin = torch.empty((n, 768), dtype=torch.uint8, device="cuda")
+    exp = torch.empty((n,), dtype=torch.uint8, device="cuda")
+    ctx.bn256_synth_checks_dev(5001, pin, exp)
+    torch.cuda.synchronize()
+    off = np.arange(n + 1, dtype=np.uint64) * 768
+    ctx.set_pipeline_depth(depth)
+    try:
+        ctx.pairing_prepare(off)
+    finally:
+        ctx.set_pipeline_depth(1)
+    ss = ctx.pipeline_streams(depth)
+    assert len({int(s.cuda_stream) for s in ss}) == depth and all(int(s.cuda_stream) for s in ss)
+    vs = [torch.full((n,), 9, dtype=torch.uint8, device="cuda") for _ in range(depth)]
+    p2 = torch.zeros_like(pin)
+    torch.cuda.synchronize()
+    p2.copy_(pin)  # default stream, no explicit synchronisation before the pipelined calls
+    for i in range(2 * depth):
+        ctx.pairing_check_batch_dev(p2, off, vs[i % depth], stream=ss[i % depth], prepare=False)
+    for s in ss:
+        s.synchronize()
+    ctx.destroy_streams(ss)
+    assert all(torch.equal(v, exp) for v in vs)

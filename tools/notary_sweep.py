@@ -34,7 +34,7 @@ def main():
             ctx.set_pipeline_depth(depth)
             ctx.notary_prepare(off, max_txs=TXS)
             ctx.set_pipeline_depth(1)
-            ss = [torch.cuda.Stream() for _ in range(depth)]
+            ss = ctx.pipeline_streams(depth)  # hardware queues of their own (gsv_stream_create)
             outs = [(torch.empty((n, 32), dtype=torch.uint8, device="cuda"),
                      torch.empty((n,), dtype=torch.int32, device="cuda"),
                      torch.empty((n, TXS // 8), dtype=torch.uint8, device="cuda"),
@@ -60,6 +60,7 @@ def main():
             torch.cuda.synchronize()
             ctx.set_timing(False)
             kt = ctx.kernel_time(_lib.K_NOTARY)[0]
+            ctx.destroy_streams(ss)
             print(f"shards {n:4d} depth {depth}: {dt * 1e3:7.3f} ms per step  {n / dt:9.1f} shards/s  "
                   f"tx kernels {kt:.3f} ms", flush=True)
 

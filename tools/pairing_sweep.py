@@ -67,7 +67,10 @@ if os.environ.get("SWEEP_CASES"):  # e.g. "4,,1;2,,1" = k,final3,miller2 (empty 
                   for c in os.environ["SWEEP_CASES"].split(";"))
 
 
-def run_pipelined(ctx, n, depth, steps=12):
+_STREAMS = []
+
+
+def run_pipelined(ctx, n, depth, steps=12, streams=None):
     """n checks per batch, consecutive batches over `depth` streams (gsv_ctx_set_pipeline_depth)"""
     if not os.environ.get("SWEEP_KEEP_LAYOUT"):  # else the GSV_BN_* overrides in the environment apply
         for v in ("GSV_BN_PAIRS_PER_LANE", "GSV_BN_FINAL3", "GSV_BN_MILLER2"):
@@ -80,7 +83,17 @@ def run_pipelined(ctx, n, depth, steps=12):
     ctx.set_pipeline_depth(depth)
     ctx.pairing_prepare(off)
     ctx.set_pipeline_depth(1)
-    ss = [torch.cuda.Stream() for _ in range(depth)]
+    global _STREAMS
+    if streams is not None:
+        ss = streams
+    elif os.environ.get("SWEEP_REUSE_STREAMS") and len(_STREAMS) >= depth:
+        ss = _STREAMS[:depth]  # the same HIP streams as the previous run
+    elif os.environ.get("SWEEP_TORCH_STREAMS"):  # torch's pool streams (may share a hardware queue)
+        ss = [torch.cuda.Stream() for _ in range(depth)]
+        _STREAMS = ss
+    else:  # streams on hardware queues of their own (gsv_stream_create), as bench.py
+        ss = ctx.pipeline_streams(depth)
+        _STREAMS = ss
     pv = [torch.empty((n,), dtype=torch.uint8, device="cuda") for _ in range(depth)]
     for i in range(depth):
         ctx.pairing_check_batch_dev(pin, off, pv[i], stream=ss[i], prepare=False)
@@ -95,7 +108,13 @@ def run_pipelined(ctx, n, depth, steps=12):
     for i in range(steps):
         ctx.pairing_check_batch_dev(pin, off, pv[i % depth], stream=ss[i % depth], prepare=False)
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps
+    dt = (time.perf_counter() - t0) / steps
+    if streams is None and not os.environ.get("SWEEP_REUSE_STREAMS"):
+        # a process's dedicated queues stay few: dozens of them (idle ones included) oversubscribe the
+        # hardware scheduler and every run slows (r05: 8,192 checks three deep 8.6 vs 3.8 ms per batch)
+        ctx.destroy_streams(ss)
+        _STREAMS = []
+    return dt
 
 
 def preheat(ctx, seconds=1.5):
@@ -118,6 +137,26 @@ def main():
     ctx = gsv.default_context()
     if os.environ.get("SWEEP_PREHEAT"):
         preheat(ctx)
+    if os.environ.get("SWEEP_STREAM_SETS"):  # e.g. "0,1,2;3,4,5": pipelines over chosen pool streams
+        if os.environ.get("SWEEP_CUMASK"):  # streams on queues of their own (a CU mask of every CU)
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            cus = torch.cuda.get_device_properties(0).multi_processor_count
+            mask = (ctypes.c_uint32 * ((cus + 31) // 32))(*([0xFFFFFFFF] * ((cus + 31) // 32)))
+            pool = []
+            for _ in range(int(os.environ["SWEEP_CUMASK"])):
+                h = ctypes.c_void_p()
+                assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), len(mask), mask) == 0
+                pool.append(torch.cuda.ExternalStream(h.value))
+        else:
+            pool = [torch.cuda.Stream() for _ in range(16)]
+        print("pool streams:", " ".join(hex(s_.cuda_stream) for s_ in pool), flush=True)
+        for n in sizes:
+            for st in os.environ["SWEEP_STREAM_SETS"].split(";"):
+                ix = [int(x) for x in st.split(",")]
+                dt = run_pipelined(ctx, n, len(ix), streams=[pool[i] for i in ix])
+                print(f"streams {st:>10} checks {n:6d} depth {len(ix)}: {dt * 1e3:8.2f} ms per batch", flush=True)
+        return
     if os.environ.get("SWEEP_PIPELINE"):  # e.g. "1,2,3": pipeline depths at auto layout
         for n in sizes:
             for d in (int(x) for x in os.environ["SWEEP_PIPELINE"].split(",")):

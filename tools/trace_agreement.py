@@ -37,7 +37,7 @@ def main(root):
         if not rows:
             continue
         prof_ms = float(rows[0]["AverageNs"]) / 1e6
-        out[key] = {"kernel": kname, "bench_hip_event_ms": bench_ms, "rocprofv3_avg_ms": round(prof_ms, 4),
+        out[key] = {"kernel": rows[0]["Name"].split("(")[0], "bench_hip_event_ms": bench_ms, "rocprofv3_avg_ms": round(prof_ms, 4),
                     "calls": int(rows[0]["Calls"]), "ratio": round(bench_ms / prof_ms, 4)}
     json.dump(out, sys.stdout, indent=1)
     print()
