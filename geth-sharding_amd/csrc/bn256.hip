@@ -968,6 +968,150 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     fp12_store(fv, nlanes, c, f);
 }
 
+// ---- the loop at TWO waves per SIMD with the line in LDS (k_bn_miller_l; GSV_BN_MILLER_L = 1).  A lane
+// has 54 words of LDS ([word][lane], 13.8 KB per wave, 110 KB for the eight waves of a CU) that hold, in
+// turn: the line (HBM -> LDS by global_load_lds_dword, no VGPRs on the way), then new.y of the line
+// product while its second sparse product runs, and v0 of the squaring while (x + y)(tau x + y) runs.
+// The formulas are mul_line_i's / fp12_sqr_i's Karatsuba, ordered so that at most about 245 registers
+// are live: line product a2 = f.x (a tau + b); s = f.x + f.y; t3 = f.y c; (a, b + c to registers; new.y
+// = t3 + tau a2 to LDS); d = a2 + t3; new.x = s (a tau + b + c) - d — the same field elements
+// (s (..) - a2 - t3 = s (..) - d); squaring v0 = f.x f.y to LDS; t = tau f.x + f.y; s = f.x + f.y;
+// new.y = s t - v0 - tau v0; new.x = 2 v0.
+typedef __attribute__((address_space(3))) uint32_t lds_w;
+GSV_DI fq ll_get(const lds_w* l, int j) {
+    fq r;
+#pragma unroll
+    for (int w = 0; w < 9; w++) r.v[w] = l[(j * 9 + w) * 64];
+    return r;
+}
+GSV_DI fp2 ll_get2(const lds_w* l, int j) { return fp2{ll_get(l, j), ll_get(l, j + 1)}; }
+GSV_DI fp6 ll_get6(const lds_w* l) { return fp6{ll_get2(l, 0), ll_get2(l, 2), ll_get2(l, 4)}; }
+GSV_DI void ll_put6(lds_w* l, const fp6& v) {
+    const uint32_t* w = (const uint32_t*)&v;
+#pragma unroll
+    for (int q = 0; q < 54; q++) l[q * 64] = w[q];
+}
+// line li of pair j (word q at lines[(li * 54 + q) * n + j]) -> LDS row q of this wave ([word][lane])
+GSV_DI void line_fetch_lds(lds_w* row0, const uint32_t* __restrict__ lines, uint32_t n, uint32_t j, int li) {
+    const uint32_t row = (uint32_t)(uintptr_t)row0;
+    const uint32_t* wb = lines + (size_t)li * 54u * n;
+#pragma unroll
+    for (int q = 0; q < 54; q++)
+        asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(j * 4u), "s"(wb + (size_t)q * n),
+                     "s"(row + (uint32_t)q * 256u)
+                     : "memory", "m0");
+}
+GSV_DI void line_lds_wait() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    asm volatile("" ::: "memory");
+}
+// an opaque copy of the lane's LDS pointer: loads through it are not merged with earlier ones, so a
+// value read twice is not held live in between
+template <class T>
+GSV_DI T* ll_fresh(T* l) {
+    asm volatile("" : "+v"(l));
+    return l;
+}
+#ifdef LL_MARKS
+#define LL_STR2(x) #x
+#define LL_STR(x) LL_STR2(x)
+#define LL_SEQ __builtin_amdgcn_sched_barrier(0); asm volatile("; LLMARK " LL_STR(__LINE__)); __builtin_amdgcn_sched_barrier(0)
+#else
+#define LL_SEQ __builtin_amdgcn_sched_barrier(0)
+#endif
+GSV_DI void ll_put2(lds_w* l, int j, const fp2& v) {
+    const uint32_t* w = (const uint32_t*)&v;
+#pragma unroll
+    for (int q = 0; q < 18; q++) l[(j * 9 + q) * 64] = w[q];
+}
+GSV_DI void mul_line_l(fp12& f, lds_w* l) {
+    fp6 a2 = fp6_store(fp6_mul_sparse(f.x, ll_get2(ll_fresh(l), 0), ll_get2(ll_fresh(l), 2)));  // f.x (a tau + b)
+    LL_SEQ;
+    f.x = fp6_store(fp6_add(f.x, f.y));  // s
+    LL_SEQ;
+    fp6 t3 = fp6_store(fp6_mul_fp2(f.y, ll_get2(ll_fresh(l), 4)));  // f.y c
+    LL_SEQ;
+    const lds_w* p = ll_fresh(l);
+    const fp2 la = ll_get2(p, 0);
+    const fp2 bc = s2(fp2_add(ll_get2(p, 2), ll_get2(p, 4)));
+    LL_SEQ;
+    // new.y = t3 + tau a2 = (t3.x + a2.y, t3.y + a2.z, t3.z + xi a2.x) -> LDS (over the line), one
+    // coordinate at a time, then d = a2 + t3 in place
+    ll_put2(ll_fresh(l), 0, s2(fp2_add(t3.x, a2.y)));
+    LL_SEQ;
+    ll_put2(ll_fresh(l), 2, s2(fp2_add(t3.y, a2.z)));
+    LL_SEQ;
+    ll_put2(ll_fresh(l), 4, s2(fp2_add(t3.z, fp2_mul_xi(a2.x))));
+    LL_SEQ;
+    a2 = fp6_store(fp6_add(a2, t3));  // d
+    LL_SEQ;
+    f.x = fp6_store(fp6_sub(fp6_mul_sparse(f.x, la, bc), a2));  // s (a tau + b + c) - d
+    LL_SEQ;
+    f.y = ll_get6(ll_fresh(l));
+}
+GSV_DI void sqr_l(fp12& f, lds_w* l) {
+    ll_put6(ll_fresh(l), fp6_store(fp6_mulx(f.x, f.y)));  // v0 -> LDS
+    LL_SEQ;
+    fp6 t = fp6_store(fp6_add(fp6_mul_tau(f.x), f.y));
+    f.x = fp6_store(fp6_add(f.x, f.y));  // s
+    fp6 st = fp6_store(fp6_mulx(f.x, t));
+    LL_SEQ;
+    fp6 v0 = ll_get6(ll_fresh(l));
+    f.y = fp6_store(fp6_sub(fp6_sub(st, v0), fp6_mul_tau(v0)));
+    f.x = fp6_store(fp6_add(v0, v0));
+}
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_bn_miller_l(
+    const uint32_t* __restrict__ lane_first, uint32_t nlanes, const uint32_t* __restrict__ pidx,
+    const uint8_t* __restrict__ pstat, const uint32_t* __restrict__ lines, uint32_t npairs,
+    uint8_t* __restrict__ cstat, uint32_t* __restrict__ fv /* [108 words][nlanes] */) {
+    __shared__ uint32_t lds[54 * 64];
+    lds_w* row0 = (lds_w*)lds;
+    lds_w* l = row0 + threadIdx.x;
+    uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nlanes) return;
+    uint32_t b = lane_first[c], e = lane_first[c + 1];
+    bool bad = false, any = false;
+    for (uint32_t q = b; q < e; q++) {
+        uint8_t st = pstat[pidx[q]];
+        bad = bad || st == PS_BAD;
+        any = any || st == PS_OK;
+    }
+    cstat[c] = bad ? CS_BAD : any ? CS_OK : CS_ONE;
+    if (bad || !any) return;
+    fp12 f = fp12_one();
+    int li = 0;
+#pragma unroll 1
+    for (int i = 64; i > 0; i--) {
+        if (i != 64) sqr_l(f, l);
+        uint64_t bit = 1ull << (i - 1);
+        int nl = ((NAF_POS | NAF_NEG) & bit) ? 2 : 1;
+#pragma unroll 1
+        for (uint32_t q = b; q < e; q++) {
+            uint32_t j = pidx[q];
+            if (pstat[j] != PS_OK) continue;
+#pragma unroll 1
+            for (int k = 0; k < nl; k++) {
+                line_fetch_lds(row0, lines, npairs, j, li + k);
+                line_lds_wait();
+                mul_line_l(f, l);
+            }
+        }
+        li += nl;
+    }
+#pragma unroll 1
+    for (uint32_t q = b; q < e; q++) {
+        uint32_t j = pidx[q];
+        if (pstat[j] != PS_OK) continue;
+#pragma unroll 1
+        for (int k = 0; k < 2; k++) {
+            line_fetch_lds(row0, lines, npairs, j, li + k);
+            line_lds_wait();
+            mul_line_l(f, l);
+        }
+    }
+    fp12_store(fv, nlanes, c, f);
+}
+
 // ---- two-lane Miller step, for batches too small to give every SIMD a wave: lanes (2c, 2c+1) run
 // Miller lane c together.  Both hold the whole accumulator; each F_p^12 squaring's two F_p^6
 // products and each line product's two sparse products (plus half of its F_p^2-scalar product)
@@ -1750,6 +1894,9 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         if (timer_begin) timer_begin(tctx, GSV_K_PAIRING);
         if (layout & GSV_BN_LAYOUT_MILLER2)
             hipLaunchKernelGGL(bn::k_bn_miller2, dim3((2 * nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
+                               d_pidx, d_use, d_lines, npairs, d_lstat, d_fv);
+        else if (layout & GSV_BN_LAYOUT_MILLERL)
+            hipLaunchKernelGGL(bn::k_bn_miller_l, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,
                                d_pidx, d_use, d_lines, npairs, d_lstat, d_fv);
         else if (layout & GSV_BN_LAYOUT_MILLERW2)
             hipLaunchKernelGGL(bn::k_bn_miller_w2, dim3((nlanes + 63) / 64), dim3(64), 0, st, d_lane_first, nlanes,

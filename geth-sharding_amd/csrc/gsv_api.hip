@@ -884,6 +884,11 @@ bool bn_miller_w2() {
     if (const char* e = getenv("GSV_BN_MILLER_W2")) return atoi(e) != 0;
     return false;
 }
+// The Miller loop at two waves per SIMD with each line in LDS (k_bn_miller_l, r05; GSV_BN_MILLER_L = 1).
+bool bn_miller_l() {
+    if (const char* e = getenv("GSV_BN_MILLER_L")) return atoi(e) != 0;
+    return false;
+}
 // The lines at two waves per SIMD (k_bn_lines_w2: P and Q in LDS, coefficients stored as computed; 256
 // registers, no scratch) or at one (k_bn_lines, 256 + 125).  Measured (r05, profiles/r05/ab/lines_w2_*,
 // pipe_l*): alone at 65,536 checks 5.95 vs 6.67 ms; in the two-deep pipeline equal (19.98 vs 19.96 ms per
@@ -926,8 +931,10 @@ std::vector<uint64_t> pairing_key(const uint64_t* h_off, size_t n) {
     const char* cc = getenv("GSV_BN_CONC");
     const char* w2 = getenv("GSV_BN_MILLER_W2");
     const char* lw = getenv("GSV_BN_LINES_W2");
+    const char* ml = getenv("GSV_BN_MILLER_L");
     std::vector<uint64_t> key{k ? (uint64_t)atoi(k) + 1 : 0, f ? (uint64_t)atoi(f) + 1 : 0, m ? (uint64_t)atoi(m) + 1 : 0,
-                              cc ? (uint64_t)atoi(cc) + 1 : 0, w2 ? (uint64_t)atoi(w2) + 1 : 0, lw ? (uint64_t)atoi(lw) + 1 : 0};
+                              cc ? (uint64_t)atoi(cc) + 1 : 0, w2 ? (uint64_t)atoi(w2) + 1 : 0, lw ? (uint64_t)atoi(lw) + 1 : 0,
+                              ml ? (uint64_t)atoi(ml) + 1 : 0};
     key.insert(key.end(), h_off, h_off + n + 1);
     return key;
 }
@@ -997,7 +1004,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
                (bn_miller2(s.nl, cus, depth) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
                (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0) | (bn_miller_w2() ? gsv::GSV_BN_LAYOUT_MILLERW2 : 0) |
-               (bn_lines_w2(np, cus) ? gsv::GSV_BN_LAYOUT_LINESW2 : 0);
+               (bn_lines_w2(np, cus) ? gsv::GSV_BN_LAYOUT_LINESW2 : 0) | (bn_miller_l() ? gsv::GSV_BN_LAYOUT_MILLERL : 0);
     s.o_src = L.add(np * 8 + 8);
     s.o_pidx = L.add(np * 4 + 4);
     s.o_lfirst = L.add((s.nl + 1) * 4);

@@ -56,7 +56,7 @@ hipError_t launch_header_verify(const uint8_t* d_sid32, const uint8_t* d_root32,
 // layout flags of launch_bn256_pairing: the final exponentiation on three lanes per check, the Miller
 // loop on two lanes per Miller lane (both for batches below one wave per SIMD)
 constexpr int GSV_BN_LAYOUT_FINAL3 = 1, GSV_BN_LAYOUT_MILLER2 = 2, GSV_BN_LAYOUT_CONC = 4, GSV_BN_LAYOUT_MILLERW2 = 8,
-              GSV_BN_LAYOUT_LINESW2 = 16;
+              GSV_BN_LAYOUT_LINESW2 = 16, GSV_BN_LAYOUT_MILLERL = 32;
 // the concurrent layout's side stream, fork/join events and the lines role's per-pair use flags
 struct BnConcurrent {
     hipStream_t side;

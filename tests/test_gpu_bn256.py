@@ -107,10 +107,12 @@ def test_pairing_miller_lane_split(ctx, oracle, monkeypatch, k):
 
 
 @pytest.mark.parametrize("k", [1, 2, 4])
-def test_pairing_two_wave_miller(ctx, oracle, monkeypatch, k):
-    """k_bn_miller_w2 (GSV_BN_MILLER_W2 = 1: one F_p^6 value per lane in LDS, products one output
-    coordinate at a time; not the default) gives the oracle's verdicts at every split."""
-    monkeypatch.setenv("GSV_BN_MILLER_W2", "1")
+@pytest.mark.parametrize("kernel", ["GSV_BN_MILLER_W2", "GSV_BN_MILLER_L"])
+def test_pairing_two_wave_miller(ctx, oracle, monkeypatch, k, kernel):
+    """The two-wave Miller kernels give the oracle's verdicts at every split: k_bn_miller_w2
+    (GSV_BN_MILLER_W2 = 1: one F_p^6 value per lane in LDS, products one output coordinate at a time)
+    and k_bn_miller_l (GSV_BN_MILLER_L = 1: the line, then new.y / v0, in LDS); neither is the default."""
+    monkeypatch.setenv(kernel, "1")
     monkeypatch.setenv("GSV_BN_MILLER2", "0")
     monkeypatch.setenv("GSV_BN_PAIRS_PER_LANE", str(k))
     inputs = _random_inputs(oracle, 71 + k)
@@ -119,7 +121,7 @@ def test_pairing_two_wave_miller(ctx, oracle, monkeypatch, k):
     assert (out == want).all(), [(i, int(out[i]), int(want[i])) for i in np.nonzero(out != want)[0]]
 
 
-@pytest.mark.parametrize("layout", ["auto", "k1", "k2", "k4", "final3", "final1", "miller2", "w2", "lines1"])
+@pytest.mark.parametrize("layout", ["auto", "k1", "k2", "k4", "final3", "final1", "miller2", "w2", "ml", "lines1"])
 def test_configs4_rank_batch_depth_three(ctx, monkeypatch, layout):
     """The N = 8 per-rank share of configs[4]: 8,192 checks from the configs[4] generator (seed 5000, all
     six seeded classes: G1 / G2 infinity pairs, (inf, outside-G2 Q), (inf, off-twist Q), a pair with Q
@@ -130,7 +132,7 @@ def test_configs4_rank_batch_depth_three(ctx, monkeypatch, layout):
     env = {"k1": ("GSV_BN_PAIRS_PER_LANE", "1"), "k2": ("GSV_BN_PAIRS_PER_LANE", "2"),
            "k4": ("GSV_BN_PAIRS_PER_LANE", "4"), "final3": ("GSV_BN_FINAL3", "1"),
            "final1": ("GSV_BN_FINAL3", "0"), "miller2": ("GSV_BN_MILLER2", "1"), "w2": ("GSV_BN_MILLER_W2", "1"),
-           "lines1": ("GSV_BN_LINES_W2", "0")}
+           "ml": ("GSV_BN_MILLER_L", "1"), "lines1": ("GSV_BN_LINES_W2", "0")}
     if layout in env:
         monkeypatch.setenv(*env[layout])
     n = 8192
