@@ -49,10 +49,13 @@ def test_partition_one_rank_equals_local_validation(ctx):
     assert (ntx.cpu().numpy() == txs).all() and int(rst[0]) == 0
 
 
-def test_partition_dev_pipelined_on_two_streams(ctx):
-    """Consecutive partition calls kept in flight on two streams (pipeline depth 2, as bench.py's notary
-    leg): each call's records equal the whole-batch validation.  At N > 1 the library orders their
-    all-gathers on the communicator (one-rank communicator here: the gather is a copy)."""
+@pytest.mark.parametrize("streams", ["torch", "dedicated"])
+def test_partition_dev_pipelined_on_two_streams(ctx, streams):
+    """Consecutive partition calls kept in flight on two streams (pipeline depth 2): each call's records
+    equal the whole-batch validation.  At N > 1 the library orders their all-gathers on the
+    communicator (a one-rank RCCL communicator here).  `dedicated`: the streams bench.py's notary leg
+    uses (gsv_stream_create, a hardware queue each), so the RCCL all-gather runs on them here before
+    the driver's multi-GPU run does."""
     import torch
     nsh, txs = 13, 512
     dev = torch.device("cuda", ctx.device)
@@ -69,7 +72,7 @@ def test_partition_dev_pipelined_on_two_streams(ctx):
         ctx.notary_partition_prepare(off, nsh, 1, 0, max_txs=txs)
     finally:
         ctx.set_pipeline_depth(1)
-    ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    ss = ctx.pipeline_streams(2) if streams == "dedicated" else [torch.cuda.Stream(device=dev) for _ in range(2)]
     outs = [(torch.zeros((nsh, 32), dtype=torch.uint8, device=dev), torch.zeros((nsh,), dtype=torch.int32, device=dev),
              torch.zeros((nsh, txs // 8), dtype=torch.uint8, device=dev),
              torch.full((1,), -99, dtype=torch.int32, device=dev)) for _ in range(6)]
@@ -79,6 +82,7 @@ def test_partition_dev_pipelined_on_two_streams(ctx):
         ctx.notary_validate_partition_dev(bodies_t, off, nsh, root, ntx, bm, rank_status_t=rst, max_txs=txs,
                                           stream=ss[i % 2], prepare=False)
     torch.cuda.synchronize()
+    ctx.destroy_streams(ss)
     for root, ntx, bm, rst in outs:
         assert np.array_equal(root.cpu().numpy(), want[0]) and np.array_equal(bm.cpu().numpy(), want[2])
         assert (ntx.cpu().numpy() == txs).all() and int(rst[0]) == 0
