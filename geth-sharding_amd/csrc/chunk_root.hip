@@ -932,6 +932,18 @@ size_t chunk_root_scratch_bytes(const TriePlan* plan, uint32_t nbodies) {
     return (ms + rs) * nbodies + 512;
 }
 
+// Where a pipelined run's bulk kernels end (GSV_HOOK_TAIL: the next run on another instance starts its
+// bulk kernels there): right after the bottom level (r05 default), so the next batch's bottom level
+// runs beside this batch's HFULL level(s) as well as its fused top — the HFULL launch of a 100-body
+// batch is ~400 waves, under half a wave per SIMD.  configs[2] 91.4-91.6 -> 93.4-94.2 GB/s at depth 2
+// and 3 (profiles/r05/ab/chunk_tail_bottom.txt).  GSV_CHUNK_TAIL_BOTTOM = 0 marks before the top (r04).
+static bool tail_after_bottom() {
+    static const bool v = [] {
+        const char* e = getenv("GSV_CHUNK_TAIL_BOTTOM");
+        return !e || atoi(e) != 0;
+    }();
+    return v;
+}
 // all heights of the plan: per-height launches below top_h, then one fused launch
 static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipStream_t st,
                                 void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx) {
@@ -965,10 +977,11 @@ static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipSt
         if (timer_end) timer_end(tctx, kid);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+        if (bot && tail_after_bottom() && timer_begin) timer_begin(tctx, GSV_HOOK_TAIL);
     }
     if (top_h <= p.height) {
         if (p.height > TOP_MAX_H) return hipErrorInvalidValue;
-        if (timer_begin) timer_begin(tctx, GSV_HOOK_TAIL);
+        if (!tail_after_bottom() && timer_begin) timer_begin(tctx, GSV_HOOK_TAIL);
         TopLevels tl{};
         tl.h0 = top_h;
         tl.h1 = p.height;
