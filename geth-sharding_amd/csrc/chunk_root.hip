@@ -459,6 +459,73 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
     emit_hash(nd, bb, body, h);
 }
 
+// Branch-free form (GSV_BOT_OR, A/B): each child's 3-5 bytes are one 40-bit value (bytes little-endian)
+// OR-ed into two aligned 32-bit words of a prezeroed [word pair][lane] LDS buffer at its running byte
+// offset (ds_or_b32), instead of 3-5 byte stores in a three-way branch that diverges on random bytes.
+#ifndef GSV_BOT_OR
+#define GSV_BOT_OR 0
+#endif
+GSV_DI void lds_or(uint32_t* p, uint32_t v) { __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// base: the workgroup's buffer, word pair k of lane t at base[k * BOT_BLOCK + t]
+GSV_DI void do_bottom_or(const PNode& nd, const BodyBatch& bb, uint32_t body, uint64_t* base, uint32_t t) {
+    const uint8_t* src = bb.bodies + bb.body_off[body] + nd.first_i;
+    uint8_t v[16];
+    if ((((uintptr_t)src) & 15u) == 0) {
+        uint4 w = *(const uint4*)src;
+        uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = (uint8_t)(ws[j >> 2] >> (8 * (j & 3)));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = src[j];
+    }
+    uint32_t payload = 1;  // trailing empty value slot 0x80
+#pragma unroll
+    for (int j = 0; j < 16; j++) payload += v[j] == 0 ? 4u : v[j] < 128 ? 3u : 5u;
+    uint64_t* m64 = base + t;
+#pragma unroll
+    for (int k = 0; k < 11; k++) m64[k * BOT_BLOCK] = 0;
+    uint32_t* m32 = (uint32_t*)m64;
+    auto wp = [&](uint32_t w) { return m32 + (w >> 1) * (2u * BOT_BLOCK) + (w & 1u); };
+    uint32_t o;
+    if (payload < 56) {
+        lds_or(wp(0), 0xc0u + payload);
+        o = 1;
+    } else {
+        lds_or(wp(0), 0xf8u | (payload << 8));
+        o = 2;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t b = v[j];
+        const bool z = b == 0, hi = b >= 128;
+        const uint32_t lo = hi ? 0x818220c4u : z ? 0x808120c3u : (0x20c2u | (b << 16));
+        const uint64_t e = (((uint64_t)(hi ? b : 0u) << 32) | lo) << ((o & 3u) * 8u);
+        lds_or(wp(o >> 2), (uint32_t)e);
+        lds_or(wp((o >> 2) + 1u), (uint32_t)(e >> 32));
+        o += hi ? 5u : z ? 4u : 3u;
+    }
+    {  // the empty value slot 0x80, then the sponge's 0x01 pad (single block: length <= 83 < 136)
+        const uint64_t e = (uint64_t)0x0180u << ((o & 3u) * 8u);
+        lds_or(wp(o >> 2), (uint32_t)e);
+        lds_or(wp((o >> 2) + 1u), (uint32_t)(e >> 32));
+    }
+    uint64_t a[25];
+#pragma unroll
+    for (int k = 0; k < 11; k++) a[k] = m64[k * BOT_BLOCK];
+#pragma unroll
+    for (int k = 11; k < 25; k++) a[k] = 0;
+    a[16] ^= 0x8000000000000000ULL;
+    keccakf(a);
+    uint32_t h[8];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        h[2 * k] = (uint32_t)a[k];
+        h[2 * k + 1] = (uint32_t)(a[k] >> 32);
+    }
+    emit_hash(nd, bb, body, h);
+}
+
 // ---------------------------------------------------------------- HFULL: 16 hashed children
 constexpr int HF_LEN = 532;
 constexpr bool hf_is_const(int p) { return p < 3 || p >= HF_LEN - 1 || (p - 3) % 33 == 0; }
@@ -829,7 +896,11 @@ __global__ __launch_bounds__(256) GSV_LEVEL_ATTR void k_chunk_level(const PNode*
     if (t >= (uint64_t)L.nn * bb.nbodies) return;
     uint32_t body = (uint32_t)(t / (uint64_t)L.nn);
     const PNode nd = nodes[L.n0 + (int)(t % (uint64_t)L.nn)];
+#if GSV_BOT_OR
+    if constexpr (BOT) do_bottom_or(nd, bb, body, sbuf, threadIdx.x);
+#else
     if constexpr (BOT) do_bottom(nd, bb, body, (uint8_t*)sbuf + threadIdx.x * BOT_BUF);
+#endif
     else do_hfull(nd, bb, body);
 }
 
