@@ -65,7 +65,10 @@ KECCAK_VALU_FLOOR_PER_PERM = 24 * 180
 # v_alignbyte) at half, 4.22.  The compiled round is 70 v_bitop3 + 62 v_xor + 58 v_alignbit
 # (ISA of k_chunk_level<BOTTOM>), so a permutation holds a SIMD >= 24 x 553 cycles: the `frac_mix_ceiling`
 # denominator, the rate a kernel doing nothing but this round could reach.
-KECCAK_ROUND_MIX = {"v_bitop3_b32": (70, 2.31), "v_xor_b32": (62, 2.37), "v_alignbit_b32": (58, 4.22)}
+# the compiled round (ISA of k_chunk_level<BOTTOM>, r05 with theta applied as one three-input XOR per
+# word, GSV_KECCAK_THETA3): 120 v_bitop3 + 2 v_xor + 58 v_alignbit = the 180-instruction floor's count
+# (r04: 70 + 62 + 58 with theta's D computed first)
+KECCAK_ROUND_MIX = {"v_bitop3_b32": (120, 2.31), "v_xor_b32": (2, 2.37), "v_alignbit_b32": (58, 4.22)}
 KECCAK_MIX_CYCLES_PER_PERM = 24 * sum(n * c for n, c in KECCAK_ROUND_MIX.values())
 # Peaks (tools/microbench_{int,lat,occ}.hip on MI355X: profiles/r01_microbench_int.txt,
 # profiles/r05/microbench_occ_ops.txt):
@@ -126,8 +129,9 @@ def mix_ceiling(units_per_launch, ms):
     compiled round's instructions at their measured SIMD cycles), beside the fixed instruction floor."""
     peak = SIMDS * 64 * CLOCK / KECCAK_MIX_CYCLES_PER_PERM
     out = {"mix_ceiling": round(peak / 1e9, 3), "mix_cycles_per_permutation": round(KECCAK_MIX_CYCLES_PER_PERM),
-           "mix_basis": "24 rounds x (70 v_bitop3 x 2.31 + 62 v_xor x 2.37 + 58 v_alignbit x 4.22) SIMD-cycles, "
-                        "profiles/r05/microbench_occ_ops.txt"}
+           "mix_basis": "24 rounds x (" + " + ".join(f"{n} {k.replace('_b32', '')} x {c}" for k, (n, c) in
+                                                     KECCAK_ROUND_MIX.items()) +
+                        ") SIMD-cycles, profiles/r05/microbench_occ_ops.txt"}
     if ms:
         out["frac_mix_ceiling"] = round(units_per_launch / (ms * 1e-3) / peak, 4)
     return out

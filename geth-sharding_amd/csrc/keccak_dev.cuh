@@ -51,17 +51,29 @@ GSV_DI void krot(uint32_t& olo, uint32_t& ohi, uint32_t lo, uint32_t hi) {
 __device__ constexpr int KECCAK_RHO[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
                                            25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
 
+// theta's D[x] = C[x - 1] ^ rot(C[x + 1], 1) is applied as ONE three-input XOR per word,
+// A ^ C[x - 1] ^ rot(C[x + 1], 1) (GSV_KECCAK_THETA3 = 1, r05): 50 v_bitop3 instead of 10 v_xor for D
+// plus 50 v_xor, i.e. the round at the 180-instruction floor.  0: D first (through r04).
+#ifndef GSV_KECCAK_THETA3
+#define GSV_KECCAK_THETA3 1
+#endif
 template <int I>
 GSV_DI void theta_rho_pi(uint32_t bl[25], uint32_t bh[25], const uint32_t al[25], const uint32_t ah[25],
-                         const uint32_t dl[5], const uint32_t dh[5]) {
+                         const uint32_t dl[5], const uint32_t dh[5], const uint32_t cl[5], const uint32_t ch[5]) {
     constexpr int x = I % 5, y = I / 5;
     constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
+#if GSV_KECCAK_THETA3
+    // dl / dh hold rot(C[x + 1], 1) here
+    krot<KECCAK_RHO[I]>(bl[dst], bh[dst], kxor3(al[I], cl[(x + 4) % 5], dl[x]), kxor3(ah[I], ch[(x + 4) % 5], dh[x]));
+#else
     krot<KECCAK_RHO[I]>(bl[dst], bh[dst], al[I] ^ dl[x], ah[I] ^ dh[x]);
-    if constexpr (I + 1 < 25) theta_rho_pi<I + 1>(bl, bh, al, ah, dl, dh);
+#endif
+    if constexpr (I + 1 < 25) theta_rho_pi<I + 1>(bl, bh, al, ah, dl, dh, cl, ch);
 }
 
 // One full permutation over the state split into 32-bit halves (lane index x + 5y).  Per round:
-// theta's column parities as 20 three-way v_bitop3, rho as 48 v_alignbit, chi as 50 v_bitop3.
+// theta's column parities as 20 three-way v_bitop3, rot(C, 1) as 10 v_alignbit, theta's application as
+// 50 three-way v_bitop3, rho as 48 v_alignbit, chi as 50 v_bitop3, iota 2.
 GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) {
 #pragma unroll 1
     for (int round = 0; round < 24; round++) {
@@ -75,11 +87,16 @@ GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) {
         for (int x = 0; x < 5; x++) {
             uint32_t rl, rh;
             krot<1>(rl, rh, cl[(x + 1) % 5], ch[(x + 1) % 5]);
+#if GSV_KECCAK_THETA3
+            dl[x] = rl;
+            dh[x] = rh;
+#else
             dl[x] = cl[(x + 4) % 5] ^ rl;
             dh[x] = ch[(x + 4) % 5] ^ rh;
+#endif
         }
         uint32_t bl[25], bh[25];
-        theta_rho_pi<0>(bl, bh, al, ah, dl, dh);
+        theta_rho_pi<0>(bl, bh, al, ah, dl, dh, cl, ch);
 #pragma unroll
         for (int y = 0; y < 25; y += 5) {
 #pragma unroll
