@@ -299,3 +299,45 @@ def test_pipeline_depth_instances_run_concurrently_and_agree(ctx, oracle):
     # re-preparing at depth 1 keeps the two-instance shapes (a higher depth is never dropped)
     ctx.chunk_root_prepare(h_off)
     assert ctx.prepared_shapes() == (n1, b1)
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_notary_dev_with_side_stream_captures_into_a_hip_graph(ctx, depth):
+    """The notary's _dev call forks its chunk roots onto a side stream (r05: the context's side streams
+    sit on hardware queues of their own, CU-masked streams) and joins them by events: the call still
+    records into a HIP graph without building anything, and the replay equals the eager results."""
+    import torch
+    nsh, txs = 3, 256
+    dev = torch.device("cuda", ctx.device)
+    bodies = torch.empty(nsh * txs * 128, dtype=torch.uint8, device=dev)
+    ctx.notary_synth_dev(91, 0, nsh, txs, bodies)
+    torch.cuda.synchronize()
+    off = np.arange(nsh + 1, dtype=np.uint64) * txs * 128
+    ctx.set_pipeline_depth(depth)
+    try:
+        ctx.notary_prepare(off, max_txs=txs)
+    finally:
+        ctx.set_pipeline_depth(1)
+    outs = [torch.zeros((nsh, 32), dtype=torch.uint8, device=dev), torch.zeros((nsh,), dtype=torch.int32, device=dev),
+            torch.zeros((nsh, txs // 8), dtype=torch.uint8, device=dev), torch.zeros((nsh, txs), dtype=torch.uint8, device=dev)]
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream()
+    shapes_before = ctx.prepared_shapes()
+    with torch.cuda.graph(g, stream=cs):
+        ctx.notary_validate_shards_dev(bodies, off, outs[0], outs[1], outs[2], None, outs[3], max_txs=txs, stream=cs,
+                                       prepare=False)
+    assert ctx.prepared_shapes() == shapes_before
+    g.replay()
+    torch.cuda.synchronize()
+    got = [t.clone() for t in outs]
+    for t in outs:
+        t.zero_()
+    es = torch.cuda.Stream()
+    es.wait_stream(torch.cuda.current_stream())
+    ctx.notary_validate_shards_dev(bodies, off, outs[0], outs[1], outs[2], None, outs[3], max_txs=txs, stream=es,
+                                   prepare=False)
+    es.synchronize()
+    for a, b in zip(got, outs):
+        assert torch.equal(a, b)
+    assert (outs[1].cpu().numpy() == txs).all()

@@ -5,6 +5,7 @@ set -o pipefail
 export PYTHONUNBUFFERED=1
 O=gpurun_out/r05aa; mkdir -p $O
 T="timeout -k 10"
+$T 300 python -u -m pytest -x -v --timeout 160 --timeout-method thread -m gpu tests/test_gpu_boundary.py -k "capture" > $O/tests_capture.log 2>&1; echo "capture tests rc=$?"; grep -E "PASS|FAIL|Error|error" $O/tests_capture.log | head -12
 for v in lw5 ku2; do
   GSV_LIB_PATH=variants/$v/libgsv.so $T 300 python -u -m pytest -x -q --timeout 160 --timeout-method thread -m gpu tests/test_gpu_chunk_root.py tests/test_gpu_keccak.py > $O/tests_$v.log 2>&1; rc=$?; tail -1 $O/tests_$v.log; [ $rc -eq 0 ] || exit $rc
 done
