@@ -376,7 +376,15 @@ GSV_DI void emit_hash(const PNode& nd, const BodyBatch& bb, uint32_t body, const
 #define GSV_BOT_PREZERO 1
 #endif
 constexpr int BOT_BLOCK = 256;
-constexpr int BOT_BUF = 96;
+// a lane's message buffer stride in LDS (bytes, a multiple of 8, >= 88): 96 = 24 words put the 64
+// lanes of a wave on 4 of the 32 banks (8-way conflicts for the 64-bit accesses); 88 (22 words) spreads
+// them over 16.  r05: bottom level 0.80 vs 0.82 ms, configs[2] equal within noise
+// (profiles/r05/ab/bottom_lds_stride.txt).  GSV_BOT_BUF overrides (A/B).
+#ifndef GSV_BOT_BUF
+#define GSV_BOT_BUF 88
+#endif
+constexpr int BOT_BUF = GSV_BOT_BUF;
+static_assert(BOT_BUF % 8 == 0 && BOT_BUF >= 88, "the 88-byte window, 8-byte aligned");
 
 // m: this lane's BOT_BUF-byte LDS buffer (8-byte aligned)
 GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8_t* m) {
