@@ -141,3 +141,48 @@ def test_sender_batch_recover_plain(ctx, oracle):
             assert st[i] == want, (i, homestead)
             if want == 0:
                 assert bytes(addr[i]) == out.raw
+
+
+def test_ecrecover_large_differential_vs_oracle(ctx, oracle):
+    """131,072 signatures through the batch API against the oracle restatement (16 host threads), bit
+    for bit: GPU-signed valid signatures, the same with recid flipped (a different, valid point or a
+    non-residue), s -> n - s (high s: ecrecover accepts it, the key changes), r and s replaced by random
+    values below n / at n and above / zero, recids 0..3 and out of range, and messages of all zeros and
+    ones.  Status and public key must match for every item."""
+    n = 1 << 17
+    msg, sig, _, _ = ctx.synth_sign(20251018, n, want_pub=False, want_addr=False)
+    rng = np.random.default_rng(77)
+    kind = rng.integers(0, 8, n)
+    sig = sig.copy()
+    msg = msg.copy()
+    be = lambda v: np.frombuffer(int(v).to_bytes(32, "big"), np.uint8)
+    nb = be(N_ORDER)
+    for i in np.nonzero(kind == 1)[0]:  # recid flipped
+        sig[i, 64] ^= 1
+    for i in np.nonzero(kind == 2)[0]:  # high s
+        s = int.from_bytes(sig[i, 32:64].tobytes(), "big")
+        sig[i, 32:64] = be(N_ORDER - s)
+    idx = np.nonzero(kind == 3)[0]  # random r, s below 2^256, recid 0..3
+    sig[idx, :64] = rng.integers(0, 256, (idx.size, 64), dtype=np.uint8)
+    sig[idx, 64] = rng.integers(0, 4, idx.size)
+    for j, i in enumerate(np.nonzero(kind == 4)[0]):  # r or s at the edges: 0, n, n + 1, 2^256 - 1
+        edge = [be(0), nb, be(N_ORDER + 1), np.full(32, 255, np.uint8)][j % 4]
+        if j % 2:
+            sig[i, :32] = edge
+        else:
+            sig[i, 32:64] = edge
+    idx = np.nonzero(kind == 5)[0]  # recid out of range
+    sig[idx, 64] = rng.choice(np.array([4, 5, 27, 28, 255], np.uint8), idx.size)
+    idx = np.nonzero(kind == 6)[0]  # the message replaced (valid r, s: another key, same status rules)
+    msg[idx] = rng.integers(0, 256, (idx.size, 32), dtype=np.uint8)
+    idx = np.nonzero(kind == 7)[0]
+    msg[idx[::2]] = 0
+    msg[idx[1::2]] = 255
+    pub, _, st = ctx.ecrecover_batch(msg, sig, want_pub=True, want_addr=False)
+    opub, ost = oracle.ecrecover_batch(msg, sig, threads=16)
+    bad = np.nonzero(st != ost)[0]
+    assert bad.size == 0, [(int(i), int(kind[i]), int(st[i]), int(ost[i])) for i in bad[:10]]
+    assert (pub == opub).all()
+    # every class produced what it should: valid ones mostly valid, out-of-range recids all rejected
+    assert (st[kind == 0] == 0).all() and (st[kind == 5] != 0).all()
+    assert len(set(st.tolist())) >= 3
