@@ -566,34 +566,78 @@ GSV_DI void hf_absorb(uint32_t al[25], uint32_t ah[25], const uint32_t* win, std
     ((al[K] ^= hf_word<B, 2 * K>(win), ah[K] ^= hf_word<B, 2 * K + 1>(win)), ...);
 }
 template <int B>
-GSV_DI void hf_block(uint32_t al[25], uint32_t ah[25], const uint4* __restrict__ Hq) {
-    constexpr int s0 = hf_s0(B), ns = hf_s1(B) - s0 + 1;
-    uint32_t win[ns * 8];
+struct HfWin {  // the child-hash slots block B reads, as 32-bit words
+    static constexpr int s0 = hf_s0(B), ns = hf_s1(B) - s0 + 1;
+    uint32_t w[ns * 8];
+};
+template <int B>
+GSV_DI void hf_load(HfWin<B>& W, const uint4* __restrict__ Hq) {
 #pragma unroll
-    for (int s = 0; s < ns; s++) {
-        uint4 a = Hq[2 * (s0 + s)], b = Hq[2 * (s0 + s) + 1];
-        win[8 * s + 0] = a.x; win[8 * s + 1] = a.y; win[8 * s + 2] = a.z; win[8 * s + 3] = a.w;
-        win[8 * s + 4] = b.x; win[8 * s + 5] = b.y; win[8 * s + 6] = b.z; win[8 * s + 7] = b.w;
+    for (int s = 0; s < HfWin<B>::ns; s++) {
+        uint4 a = Hq[2 * (HfWin<B>::s0 + s)], b = Hq[2 * (HfWin<B>::s0 + s) + 1];
+        W.w[8 * s + 0] = a.x; W.w[8 * s + 1] = a.y; W.w[8 * s + 2] = a.z; W.w[8 * s + 3] = a.w;
+        W.w[8 * s + 4] = b.x; W.w[8 * s + 5] = b.y; W.w[8 * s + 6] = b.z; W.w[8 * s + 7] = b.w;
     }
-    hf_absorb<B>(al, ah, win, std::make_integer_sequence<int, 17>{});
+}
+// the loaded words are "used" here, so the loads stay where they were issued (before the permutation
+// they overlap) instead of being sunk to their real use
+template <int B>
+GSV_DI void hf_pin(HfWin<B>& W) {
+#pragma unroll
+    for (int k = 0; k < HfWin<B>::ns * 8; k++) asm volatile("" : "+v"(W.w[k]));
+}
+template <int B>
+GSV_DI void hf_absorb_block(uint32_t al[25], uint32_t ah[25], const HfWin<B>& W) {
+    hf_absorb<B>(al, ah, W.w, std::make_integer_sequence<int, 17>{});
     if constexpr (B == 3) {  // pad: 0x01 at byte 532 - 408 = 124 (lane 15, high half), 0x80 at byte 135
         ah[15] ^= 0x01u;
         ah[16] ^= 0x80000000u;
     }
-    keccakf_split(al, ah);
 }
+#ifndef GSV_HF_PREFETCH
+#define GSV_HF_PREFETCH 0
+#endif
 // Keccak-256 of the full branch f9 02 11 | (a0 || H_0) ... (a0 || H_15) | 80 (532 bytes, 4 blocks).
 // Every byte's source is a compile-time function of its offset (templates above), so each 32-bit
-// message word is a shift/or of at most two child-hash words held in registers — no message buffer.
+// message word is a v_perm / shift of at most two child-hash words held in registers — no message
+// buffer.  GSV_HF_PREFETCH = 1 (A/B, r05): block B + 1's child-hash words are loaded before block B's
+// permutation; measured slower (configs[2] 100.0 vs 101.3 GB/s: the held words raise the level kernel
+// to 129 VGPRs, three waves per SIMD; profiles/r05/ab/hfull_prefetch.txt), so off.
 GSV_DI void hash_hfull(uint32_t h[8], const uint32_t* __restrict__ H) {
     uint32_t al[25], ah[25];
 #pragma unroll
     for (int k = 0; k < 25; k++) al[k] = ah[k] = 0;
     const uint4* Hq = (const uint4*)H;
-    hf_block<0>(al, ah, Hq);
-    hf_block<1>(al, ah, Hq);
-    hf_block<2>(al, ah, Hq);
-    hf_block<3>(al, ah, Hq);
+    HfWin<0> w0;
+    HfWin<1> w1;
+    HfWin<2> w2;
+    HfWin<3> w3;
+    hf_load(w0, Hq);
+    hf_absorb_block(al, ah, w0);
+#if GSV_HF_PREFETCH
+    hf_load(w1, Hq);
+    hf_pin(w1);
+    keccakf_split(al, ah);
+    hf_absorb_block(al, ah, w1);
+    hf_load(w2, Hq);
+    hf_pin(w2);
+    keccakf_split(al, ah);
+    hf_absorb_block(al, ah, w2);
+    hf_load(w3, Hq);
+    hf_pin(w3);
+    keccakf_split(al, ah);
+#else
+    keccakf_split(al, ah);
+    hf_load(w1, Hq);
+    hf_absorb_block(al, ah, w1);
+    keccakf_split(al, ah);
+    hf_load(w2, Hq);
+    hf_absorb_block(al, ah, w2);
+    keccakf_split(al, ah);
+    hf_load(w3, Hq);
+#endif
+    hf_absorb_block(al, ah, w3);
+    keccakf_split(al, ah);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         h[2 * k] = al[k];
