@@ -1033,22 +1033,33 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
 // two independent launch chains at once: the pairing's concurrent layout, the notary's chunk roots
 int shape_side_init(gsv_ctx* c, Shape& s) {
     if (!s.side.empty()) return GSV_SUCCESS;
-    s.side.assign(s.ninst, nullptr);
-    s.efork.assign(s.ninst, nullptr);
-    s.ejoin.assign(s.ninst, nullptr);
-    for (int k = 0; k < s.ninst; k++) {
+    std::vector<hipStream_t> side(s.ninst, nullptr);
+    std::vector<hipEvent_t> efork(s.ninst, nullptr), ejoin(s.ninst, nullptr);
+    int rc = GSV_SUCCESS;
+    for (int k = 0; k < s.ninst && !rc; k++) {
         // instance k's side stream: the context's k-th, on a hardware queue of its own (shared by the
         // shapes: only their side chains on one instance index are ordered after each other)
-        while ((int)c->sides.size() <= k) {
+        while (!rc && (int)c->sides.size() <= k) {
             hipStream_t q = nullptr;
-            int rc = own_queue_stream(c->device, &q);
-            if (rc) return rc;
-            c->sides.push_back(q);
+            rc = own_queue_stream(c->device, &q);
+            if (!rc) c->sides.push_back(q);
         }
-        s.side[k] = c->sides[k];
-        HIPCHK(hipEventCreateWithFlags(&s.efork[k], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&s.ejoin[k], hipEventDisableTiming));
+        if (rc) break;
+        side[k] = c->sides[k];
+        if (hipEventCreateWithFlags(&efork[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ejoin[k], hipEventDisableTiming) != hipSuccess)
+            rc = GSV_E_HIP;
     }
+    if (rc) {  // no partial set: a shape without side streams runs its chains on the caller's stream
+        for (hipEvent_t e : efork)
+            if (e) hipEventDestroy(e);
+        for (hipEvent_t e : ejoin)
+            if (e) hipEventDestroy(e);
+        return rc;
+    }
+    s.side = std::move(side);
+    s.efork = std::move(efork);
+    s.ejoin = std::move(ejoin);
     return GSV_SUCCESS;
 }
 // a host-path (per-call) shape borrows the context's side stream and events instead of creating its own
