@@ -30,7 +30,7 @@ def main():
         ctx.notary_synth_dev(777, 0, n, TXS, nb, exp, None, stream=st0)
         off = np.arange(n + 1, dtype=np.uint64) * TXS * 128
         st0.synchronize()
-        for depth in (1, 2, 3):
+        for depth in tuple(int(x) for x in os.environ.get("NOTARY_DEPTHS", "1,2,3").split(",")):
             ctx.set_pipeline_depth(depth)
             ctx.notary_prepare(off, max_txs=TXS)
             ctx.set_pipeline_depth(1)
