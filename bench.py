@@ -793,9 +793,12 @@ def pipeline_streams(ctx, depth, stream, dev):
     (gsv_stream_create); GSV_BENCH_TORCH_STREAMS=1 takes the leg's stream and torch pool streams instead
     (A/B: those can share one of HIP's four in-order queues)."""
     import torch
-    if os.environ.get("GSV_BENCH_TORCH_STREAMS") == "1":
-        return [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
-    return ctx.pipeline_streams(depth)
+    if os.environ.get("GSV_BENCH_TORCH_STREAMS") != "1":
+        try:
+            return ctx.pipeline_streams(depth)
+        except Exception as e:  # a box whose HIP refuses CU-masked streams: still measure, say so
+            print(f"bench: gsv_stream_create failed ({e}); pipelines on torch streams", file=sys.stderr)
+    return [stream] + [torch.cuda.Stream(device=dev) for _ in range(depth - 1)]
 
 
 def leg_pairing(ctx, stream, dev, ws, rank, args):
