@@ -62,12 +62,11 @@ KECCAK_VALU_FLOOR_PER_PERM = 24 * 180
 # profiles/r05/microbench_occ_ops.txt, tools/microbench_occ.hip: SIMD-cycles per wave64 instruction at
 # four waves per SIMD, nominal 2.4 GHz): v_bitop3_b32 2.31 and v_xor_b32 2.37 issue at the full rate,
 # v_alignbit_b32 (like every other three-source VALU op measured: v_or3, v_add3, v_bfi, v_perm,
-# v_alignbyte) at half, 4.22.  The compiled round is 70 v_bitop3 + 62 v_xor + 58 v_alignbit
-# (ISA of k_chunk_level<BOTTOM>), so a permutation holds a SIMD >= 24 x 553 cycles: the `frac_mix_ceiling`
-# denominator, the rate a kernel doing nothing but this round could reach.
-# the compiled round (ISA of k_chunk_level<BOTTOM>, r05 with theta applied as one three-input XOR per
-# word, GSV_KECCAK_THETA3): 120 v_bitop3 + 2 v_xor + 58 v_alignbit = the 180-instruction floor's count
-# (r04: 70 + 62 + 58 with theta's D computed first)
+# v_alignbyte) at half, 4.22.  The compiled round (ISA of k_chunk_level<BOTTOM>, r05 with theta applied
+# as one three-input XOR per word, GSV_KECCAK_THETA3) is 120 v_bitop3 + 2 v_xor + 58 v_alignbit = the
+# 180-instruction floor's count (r04: 70 + 62 + 58 with theta's D computed first), so a permutation
+# holds a SIMD >= 24 x 527 cycles: the `frac_mix_ceiling` denominator, the rate a kernel doing nothing
+# but this round could reach.
 KECCAK_ROUND_MIX = {"v_bitop3_b32": (120, 2.31), "v_xor_b32": (2, 2.37), "v_alignbit_b32": (58, 4.22)}
 KECCAK_MIX_CYCLES_PER_PERM = 24 * sum(n * c for n, c in KECCAK_ROUND_MIX.values())
 # Peaks (tools/microbench_{int,lat,occ}.hip on MI355X: profiles/r01_microbench_int.txt,
