@@ -53,8 +53,10 @@ hipError_t launch_header_verify(const uint8_t* d_sid32, const uint8_t* d_root32,
                                 const uint4* gtab, uint8_t* d_scratch, uint8_t* d_hash32, uint8_t* d_signer20,
                                 uint8_t* d_status, hipStream_t st);
 
-// layout flags of launch_bn256_pairing: the final exponentiation on three lanes per check, the Miller
-// loop on two lanes per Miller lane (both for batches below one wave per SIMD)
+// layout flags of launch_bn256_pairing: the final exponentiation on three lanes per check and the Miller
+// loop on two lanes per Miller lane (batches below one wave per SIMD), the one-wave lines kernel
+// (CONC), the two-wave lines kernel (LINESW2, large batches), and the two-wave Miller kernels kept for
+// A/B (MILLERW2, MILLERL; off by default)
 constexpr int GSV_BN_LAYOUT_FINAL3 = 1, GSV_BN_LAYOUT_MILLER2 = 2, GSV_BN_LAYOUT_CONC = 4, GSV_BN_LAYOUT_MILLERW2 = 8,
               GSV_BN_LAYOUT_LINESW2 = 16, GSV_BN_LAYOUT_MILLERL = 32;
 // the concurrent layout's side stream, fork/join events and the lines role's per-pair use flags

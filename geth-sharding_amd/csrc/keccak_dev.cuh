@@ -71,15 +71,15 @@ GSV_DI void theta_rho_pi(uint32_t bl[25], uint32_t bh[25], const uint32_t al[25]
     if constexpr (I + 1 < 25) theta_rho_pi<I + 1>(bl, bh, al, ah, dl, dh, cl, ch);
 }
 
-// One full permutation over the state split into 32-bit halves (lane index x + 5y).  Per round:
-// theta's column parities as 20 three-way v_bitop3, rot(C, 1) as 10 v_alignbit, theta's application as
-// 50 three-way v_bitop3, rho as 48 v_alignbit, chi as 50 v_bitop3, iota 2.
-// rounds per loop iteration (GSV_KECCAK_UNROLL, A/B; 1 = one round per iteration)
+// rounds per loop iteration (GSV_KECCAK_UNROLL, A/B; 1 = one round per iteration; 2 measured equal, r05)
 #ifndef GSV_KECCAK_UNROLL
 #define GSV_KECCAK_UNROLL 1
 #endif
 #define GSV_PRAGMA(x) _Pragma(#x)
 #define GSV_UNROLL(n) GSV_PRAGMA(unroll n)
+// One full permutation over the state split into 32-bit halves (lane index x + 5y).  Per round:
+// theta's column parities as 20 three-way v_bitop3, rot(C, 1) as 10 v_alignbit, theta's application as
+// 50 three-way v_bitop3, rho as 48 v_alignbit, chi as 50 v_bitop3, iota 2.
 GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) {
     GSV_UNROLL(GSV_KECCAK_UNROLL)
     for (int round = 0; round < 24; round++) {
