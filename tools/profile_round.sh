@@ -2,7 +2,7 @@
 # Profiles the bench on the GPU box (run through gpurun from the repo root):
 #   all            rocprofv3 --kernel-trace --stats over the default bench      -> kernel_stats.csv
 #   per leg G in {ecrecover, chunk_root, keccak, pairing, notary}: the leg ALONE, single stream
-#   (--pipeline 1 --pairing-pipeline 1 --notary-pipeline 1, so no dispatch overlaps another batch's and the trace
+#   (--pipeline 1 --pairing-pipeline 1 --notary-pipeline 1 --ecrecover-pipeline 1, so no dispatch overlaps another batch's and the trace
 #   average is the kernel's own duration), each counter set in its own pass:
 #        --kernel-trace                                               -> durations
 #        FETCH_SIZE / WRITE_SIZE                                      -> HBM bytes per dispatch
@@ -24,7 +24,7 @@ for G in $GROUPS_; do
         find $OUT/all/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
         continue
     fi
-    B="--legs $G --steps 3 --warmup 1 --no-cpu-baseline --pipeline 1 --pairing-pipeline 1 --notary-pipeline 1"
+    B="--legs $G --steps 3 --warmup 1 --no-cpu-baseline --pipeline 1 --pairing-pipeline 1 --notary-pipeline 1 --ecrecover-pipeline 1"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -f rocpd csv -d $OUT/$G/trace -o run -- python3 bench.py $B > $OUT/$G.trace.log 2>&1 || { echo "trace pass $G failed"; exit 1; }
     find $OUT/$G/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_$G.csv \;
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/$G/fetch -o run -- python3 bench.py $B > $OUT/$G.fetch.log 2>&1 || { echo "fetch pass $G failed"; exit 1; }
