@@ -364,11 +364,9 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
         ctx.synth_sign_dev(1000 + rank, msg, sig, epub, eaddr, stream=stream)
     stream.synchronize()
 
-    # consecutive batches on two streams with hardware queues of their own, each with its own outputs
-    # (the recovery keeps no per-call state): one batch's last wave round overlaps the next batch's
-    # first; the timed region runs without kernel-timing events (an event pair per launch cost ~3 %
-    # here, r05: 117.3 vs 113.9 M/s, profiles/r05/ab/ecrecover_streams.txt) and the kernel average comes
-    # from a separate instrumented pass on one stream, as in the other legs
+    # --ecrecover-pipeline D > 1: consecutive batches on D streams with hardware queues of their own,
+    # each with its own outputs (the recovery keeps no per-call state), so one batch's last wave round
+    # overlaps the next batch's first (+1.2-1.6 % in a standalone A/B, profiles/r05/ab/ecrecover_steps.txt)
     edepth = max(1, args.ecrecover_pipeline)
     estreams = pipeline_streams(ctx, edepth, stream, dev)
     eouts = [(pub, addr, st)] + [(torch.empty_like(pub), torch.empty_like(addr), torch.empty_like(st))
@@ -388,6 +386,13 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
     for p_, a_, s2_ in eouts:
         assert int(s2_.max().item()) == 0, "recovery failed on valid signatures"
         assert torch.equal(p_, epub) and torch.equal(a_, eaddr), "recovered keys differ from signers"
+    # one stream (the default): the kernel time comes from HIP events around every launch of the timed
+    # region itself; batches in flight on several streams would overlap those event pairs, so there
+    # it comes from a separate instrumented pass on one of the (warm) streams after the timed region
+    live = edepth == 1
+    if live:
+        ctx.reset_timing()
+        ctx.set_timing(True)
     barrier(ws)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -398,18 +403,17 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
     dt = max_over_ranks(time.perf_counter() - t0, ws)
     for p_, a_, s2_ in eouts:
         assert torch.equal(p_, epub) and torch.equal(a_, eaddr), "recovered keys differ from signers"
-    # the per-launch kernel time: an instrumented pass of back-to-back launches on one of the (warm)
-    # pipeline streams; its first launch is not counted (a stream's first dispatch reads slow)
-    ctx.ecrecover_batch_dev(msg, sig, pub, addr, st, stream=estreams[0])
-    ctx.reset_timing()
-    ctx.set_timing(True)
-    for _ in range(max(4, args.steps)):
-        ctx.ecrecover_batch_dev(msg, sig, pub, addr, st, stream=estreams[0])
-    estreams[0].synchronize()
+    if not live:
+        ctx.reset_timing()
+        ctx.set_timing(True)
+        for _ in range(max(4, args.steps)):
+            ctx.ecrecover_batch_dev(msg, sig, pub, addr, st, stream=estreams[0])
+        estreams[0].synchronize()
     ctx.set_timing(False)
     ctx.destroy_streams(estreams)
     k_ms, k_n = ctx.kernel_time(_lib.K_ECRECOVER)
     k_avg_ms = max_over_ranks(k_ms / max(k_n, 1), ws)
+    k_launches = int(k_n)
     rate = ws * N_SIGS * args.steps / dt
     k = pmc("gsv::k_ecrecover", "pmc_ecrecover.json")
     ref_ach = MACS_PER_RECOVERY_REF * N_SIGS / (k_avg_ms * 1e-3)
@@ -423,6 +427,7 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
             "traffic": pmc_traffic(k),
             "traffic_source": f"profiles/{ROUND}/pmc_ecrecover.json" if pmc_traffic(k) else None,
             "profiled_kernel_avg_ms": k.get("avg_ms"),
+            "kernel_launches_timed": k_launches,  # the instrumented pass's launches (the last of the leg)
             "trace_agreement": f"profiles/{ROUND}/trace_agreement.json",
             "algorithmic_bytes_per_launch": N_SIGS * (32 + 65 + 65 + 20 + 1),
             # by design: one 80-byte affine comb entry per 20-bit window of u1 (13 per recovery) from the
@@ -1036,9 +1041,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--legs", default=",".join(LEGS), help="comma list of " + ",".join(LEGS))
-    ap.add_argument("--ecrecover-pipeline", type=int, default=2,
-                    help="streams consecutive ecrecover batches are spread over (1: one stream, as the "
-                         "leg-only profile passes run it so each trace average is a lone kernel's)")
+    ap.add_argument("--ecrecover-pipeline", type=int, default=1,
+                    help="streams consecutive ecrecover batches are spread over (1, the default: one stream, "
+                         "with the roofline's kernel time from HIP events over the timed region itself)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="streams (shape instances) consecutive chunk-root batches are spread over")
     ap.add_argument("--pairing-pipeline", type=int, default=0,

@@ -11,6 +11,7 @@ for f in opcount.json gpu_tests.log smoke.log bench.log; do
   [ -f gpurun_out/$R/$f ] && cp gpurun_out/$R/$f $P/
 done
 cp gpurun_out/prof/$R/pmc_*.json gpurun_out/prof/$R/kernel_stats*.csv $P/
+ls gpurun_out/prof/$R/dispatch_*.csv >/dev/null 2>&1 && cp gpurun_out/prof/$R/dispatch_*.csv $P/trace_logs/
 for G in ecrecover chunk_root keccak pairing notary; do
   L=gpurun_out/prof/$R/$G.trace.log
   [ -f $L ] && grep '^{' $L | tail -1 > $P/trace_logs/bench_under_trace_$G.json

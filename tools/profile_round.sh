@@ -27,6 +27,19 @@ for G in $GROUPS_; do
     B="--legs $G --steps 3 --warmup 1 --no-cpu-baseline --pipeline 1 --pairing-pipeline 1 --notary-pipeline 1 --ecrecover-pipeline 1"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -f rocpd csv -d $OUT/$G/trace -o run -- python3 bench.py $B > $OUT/$G.trace.log 2>&1 || { echo "trace pass $G failed"; exit 1; }
     find $OUT/$G/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_$G.csv \;
+    # per-dispatch start / end of the library's kernels (small): tools/trace_agreement.py compares the
+    # bench's instrumented launches with the same launches here (the first launches of a process read slow)
+    python3 - $OUT/$G/trace $OUT/dispatch_$G.csv <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)
+rows = [r for r in csv.DictReader(open(f[0]))] if f else []
+with open(sys.argv[2], "w") as o:
+    o.write("kernel,start_ns,end_ns\n")
+    for r in sorted(rows, key=lambda r: int(r["Start_Timestamp"])):
+        n = r["Kernel_Name"].split("(")[0]
+        if "gsv::" in n:
+            o.write(f"{n.replace(',', ';')},{r['Start_Timestamp']},{r['End_Timestamp']}\n")
+PY
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/$G/fetch -o run -- python3 bench.py $B > $OUT/$G.fetch.log 2>&1 || { echo "fetch pass $G failed"; exit 1; }
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/$G/write -o run -- python3 bench.py $B > $OUT/$G.write.log 2>&1 || { echo "write pass $G failed"; exit 1; }
     timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $OUT/$G/sq -o run -- python3 bench.py $B > $OUT/$G.sq.log 2>&1 || { echo "sq pass $G failed"; exit 1; }

@@ -37,8 +37,22 @@ def main(root):
         if not rows:
             continue
         prof_ms = float(rows[0]["AverageNs"]) / 1e6
-        out[key] = {"kernel": rows[0]["Name"].split("(")[0], "bench_hip_event_ms": bench_ms, "rocprofv3_avg_ms": round(prof_ms, 4),
+        kname_full = rows[0]["Name"].split("(")[0]
+        out[key] = {"kernel": kname_full, "bench_hip_event_ms": bench_ms, "rocprofv3_avg_ms": round(prof_ms, 4),
                     "calls": int(rows[0]["Calls"]), "ratio": round(bench_ms / prof_ms, 4)}
+        # the same launches on both sides where the bench names its instrumented launch count (the last
+        # launches of its leg): the trace's first launches of a process read slow (clock ramp-up)
+        try:
+            with open(os.path.join(root, "trace_logs", f"bench_under_trace_{leg}.json")) as f:
+                n = json.loads(f.read())["roofline"].get("kernel_launches_timed") if leg == "ecrecover" else None
+            with open(os.path.join(root, "trace_logs", f"dispatch_{leg}.csv")) as f:
+                d = [r for r in csv.DictReader(f) if r["kernel"] == kname_full]
+        except (OSError, KeyError, ValueError):
+            n, d = None, []
+        if n and len(d) >= n:
+            last = sum(int(r["end_ns"]) - int(r["start_ns"]) for r in d[-n:]) / n / 1e6
+            out[key].update({"rocprofv3_same_launches_ms": round(last, 4), "same_launches": n,
+                             "ratio_same_launches": round(bench_ms / last, 4)})
     json.dump(out, sys.stdout, indent=1)
     print()
 
