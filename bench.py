@@ -621,7 +621,7 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     assert torch.equal(g_root, a_root) and torch.equal(g_ntx, a_ntx) and torch.equal(g_bm, a_bm), \
         "C-ABI RCCL records differ from the torch.distributed gather"
     nsteps = max(2 * depth, args.steps // 2)
-    for i in range(1, depth):  # warm the other instances
+    for i in range(1, max(depth, args.warmup)):  # warm the other instances (at least --warmup steps)
         notary_step(i=i)
     for s_ in n_streams:
         s_.synchronize()
@@ -872,15 +872,15 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     pvk = [pver] + [torch.empty_like(pver) for _ in range(depth - 1)]
     ctx.pairing_prepare(p_off)
     ctx.set_pipeline_depth(1)
-    for i in range(depth):  # warmup
-        ctx.pairing_check_batch_dev(pin, p_off, pvk[i], stream=streams[i], prepare=False)
+    for i in range(max(depth, args.warmup)):  # warm-up (every stream, at least --warmup batches)
+        ctx.pairing_check_batch_dev(pin, p_off, pvk[i % depth], stream=streams[i % depth], prepare=False)
     for s_ in streams:
         s_.synchronize()
     # size-independent parity property at full size: every verdict equals the generator's
     assert all(torch.equal(v, pexp) for v in pvk), "pairing verdicts differ from the constructed truth"
     # small per-rank batches: enough batches that the pipeline's fill and drain (about one batch
     # latency, depth x the per-batch time) stay a small part of the timed region
-    psteps = (6 if depth <= 3 else 2 * depth) if nloc >= 65536 else 6 * depth
+    psteps = max((6 if depth <= 3 else 2 * depth) if nloc >= 65536 else 6 * depth, args.steps // 2)
     barrier(ws)
     t2 = time.perf_counter()
     for i in range(psteps):
