@@ -999,7 +999,18 @@ constexpr int TOP_BLOCK = TOP_HFULL_THREADS + 64 * TOP_GEN_WAVES;
 constexpr int TOP_GROUPS = TOP_BLOCK / 32;
 constexpr int TOP_COOP_MAX = TOP_GROUPS;  // nodes per height up to which every node is group-hashed (one round)
 
-__global__ __launch_bounds__(TOP_BLOCK) void k_chunk_top(const PNode* __restrict__ nodes,
+// register budget of the fused top (GSV_TOP_WAVES waves per SIMD, 0 = the compiler's choice, 178 VGPRs):
+// its waves sit beside the next batch's bottom level, and a smaller allocation leaves that level more
+// of each SIMD's register file (A/B)
+#ifndef GSV_TOP_WAVES
+#define GSV_TOP_WAVES 0
+#endif
+#if GSV_TOP_WAVES
+#define GSV_TOP_ATTR __attribute__((amdgpu_waves_per_eu(GSV_TOP_WAVES)))
+#else
+#define GSV_TOP_ATTR
+#endif
+__global__ __launch_bounds__(TOP_BLOCK) GSV_TOP_ATTR void k_chunk_top(const PNode* __restrict__ nodes,
                                                          const PChild* __restrict__ children, TopLevels tl,
                                                          BodyBatch bb) {
     __shared__ uint64_t gbuf[TOP_GROUPS * MSG_STRIDE / 8];
