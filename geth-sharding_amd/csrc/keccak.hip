@@ -2,6 +2,7 @@
 // sponge crypto/sha3/sha3.go:98-157, rate 136, dsbyte 0x01).  One message per lane; each lane
 // absorbs its own 136-byte blocks.  Used for transaction sighashes (RLP preimages) and as the
 // generic batch hash entry point.
+#include <stdlib.h>
 #include "gsv_internal.h"
 #include "keccak_dev.cuh"
 
@@ -83,7 +84,13 @@ __global__ __launch_bounds__(256) void k_keccak256(const uint8_t* __restrict__ d
 hipError_t launch_keccak256(const uint8_t* data, const uint64_t* off, uint32_t n, uint8_t* out32,
                             hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_keccak256, dim3((n + 255) / 256), dim3(256), 0, st, data, off, n, out32);
+    // workgroup size (GSV_KECCAK_BLOCK = 64 / 128 / 256, A/B; the bucket order works within any of them)
+    static const uint32_t blk = [] {
+        const char* e = getenv("GSV_KECCAK_BLOCK");
+        uint32_t b = e ? (uint32_t)atoi(e) : 256u;
+        return (b == 64u || b == 128u) ? b : 256u;
+    }();
+    hipLaunchKernelGGL(k_keccak256, dim3((n + blk - 1) / blk), dim3(blk), 0, st, data, off, n, out32);
     return hipGetLastError();
 }
 
