@@ -620,7 +620,12 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     g_root, g_ntx, g_bm = SH.unpack_records(gathered, ws, N_SHARDS, NOTARY_TXS)
     assert torch.equal(g_root, a_root) and torch.equal(g_ntx, a_ntx) and torch.equal(g_bm, a_bm), \
         "C-ABI RCCL records differ from the torch.distributed gather"
-    nsteps = max(2 * depth, args.steps // 2)
+    # Strong scaling: a rank's step shrinks with N (13 of the 100 shards at N = 8), so each rank times N
+    # times the steps and the timed region spans about the same wall time at every N.  A pipeline's
+    # fill and drain cost about one step's latency (~1.3 ms at 13 shards) per timed region: 12 timed
+    # 13-shard steps read 1.28 ms per step, 40 read 1.16 (the steady state; 100 shards 8.76 ms, i.e.
+    # 98 % of linear), profiles/r06/ab/notary_stagger_steps.txt
+    nsteps = max(2 * depth, args.steps // 2) * ws
     for i in range(1, max(depth, args.warmup)):  # warm the other instances (at least --warmup steps)
         notary_step(i=i)
     for s_ in n_streams:
@@ -880,7 +885,8 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     assert all(torch.equal(v, pexp) for v in pvk), "pairing verdicts differ from the constructed truth"
     # small per-rank batches: enough batches that the pipeline's fill and drain (about one batch
     # latency, depth x the per-batch time) stay a small part of the timed region
-    psteps = max((6 if depth <= 3 else 2 * depth) if nloc >= 65536 else 6 * depth, args.steps // 2)
+    # (strong scaling, as the notary leg: N times the batches at N ranks, about the same wall time)
+    psteps = max((6 if depth <= 3 else 2 * depth) if nloc >= 65536 else 6 * depth, args.steps // 2) * ws
     barrier(ws)
     t2 = time.perf_counter()
     for i in range(psteps):

@@ -53,10 +53,7 @@ namespace bn {
 constexpr uint32_t FQ_M29 = 0x1FFFFFFFu;
 constexpr int FQ_LMAX = 8;    // limbs <= 8 (2^29 - 1) < 2^32
 constexpr int FQ_VMAX = 160;  // value < 160 p: limb 8 of a normalised element stays < 2^29
-#ifndef BN_VS
-#define BN_VS 20
-#endif
-constexpr int VS = BN_VS;     // value bound of a stored element
+constexpr int VS = 20;        // value bound of a stored element
 
 template <int L, int V>
 struct fqm {
@@ -298,49 +295,10 @@ FQ_FN void fq_redc_core(uint32_t r[9], const uint32_t a[9], const uint32_t b[9],
     r[8] = (uint32_t)acc;
 }
 
-#ifndef BN_MUL_INLINE
-#define BN_MUL_INLINE 1
-#endif
 #if defined(__HIPCC__)
-// BN_MUL_INLINE 0: out of line (one copy of the ~250 instructions in the I-cache), operands and
-// result in VGPRs — but every value live across the call must sit in a callee-saved register.
-typedef uint32_t fqv __attribute__((ext_vector_type(9)));
+// out-of-line device functions (one copy in the I-cache); the F_p products themselves stay inline
+// (out of line, every value live across a call would have to sit in a callee-saved register)
 #define BN_NI __device__ __noinline__
-static BN_NI fqv fq_mul_v(fqv a, fqv b) {
-    uint32_t x[9], y[9], r[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-        x[i] = a[i];
-        y[i] = b[i];
-    }
-    fq_redc_core<false>(r, x, y, x, y);
-    fqv o;
-#pragma unroll
-    for (int i = 0; i < 9; i++) o[i] = r[i];
-    return o;
-}
-static BN_NI fqv fq_mul2_v(fqv a, fqv b, fqv c, fqv d) {
-    uint32_t x[9], y[9], z[9], w[9], r[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-        x[i] = a[i];
-        y[i] = b[i];
-        z[i] = c[i];
-        w[i] = d[i];
-    }
-    fq_redc_core<true>(r, x, y, z, w);
-    fqv o;
-#pragma unroll
-    for (int i = 0; i < 9; i++) o[i] = r[i];
-    return o;
-}
-template <int L, int V>
-FQ_FN fqv fq_tov(const fqm<L, V>& a) {
-    fqv r;
-#pragma unroll
-    for (int i = 0; i < 9; i++) r[i] = a.v[i];
-    return r;
-}
 #endif
 
 // a * b R^-1 (mod p)
@@ -356,13 +314,7 @@ FQ_FN auto fq_mul(const fqm<La, Va>& a, const fqm<Lb, Vb>& b) {
         GSV_OPC(gsv::OPC_BN_MUL);
         GSV_OPC(gsv::OPC_BN_REDC);
         fqm<1, fq_prod_v(Va, Vb)> r;
-#if defined(__HIPCC__) && !BN_MUL_INLINE
-        fqv o = fq_mul_v(fq_tov(a), fq_tov(b));
-#pragma unroll
-        for (int i = 0; i < 9; i++) r.v[i] = o[i];
-#else
         fq_redc_core<false>(r.v, a.v, b.v, a.v, b.v);
-#endif
         return r;
     }
 }
@@ -383,13 +335,7 @@ FQ_FN auto fq_mul2(const fqm<La, Va>& a, const fqm<Lb, Vb>& b, const fqm<Lc, Vc>
         GSV_OPC(gsv::OPC_BN_MUL);
         GSV_OPC(gsv::OPC_BN_REDC);
         fqm<1, (Va * Vb + Vc * Vd) / 168 + 2> r;
-#if defined(__HIPCC__) && !BN_MUL_INLINE
-        fqv o = fq_mul2_v(fq_tov(a), fq_tov(b), fq_tov(c), fq_tov(d));
-#pragma unroll
-        for (int i = 0; i < 9; i++) r.v[i] = o[i];
-#else
         fq_redc_core<true>(r.v, a.v, b.v, c.v, d.v);
-#endif
         return r;
     }
 }

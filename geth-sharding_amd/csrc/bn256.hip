@@ -3,7 +3,7 @@
 //
 // One lane per pair for decode + G2 subgroup check, one lane per check for the multi-Miller loop
 // and the final exponentiation.  Three launches:
-//   k_bn_prepare  two wave roles per 64 pairs, running concurrently:
+//   k_bn_lines    (or k_bn_lines_w2, large batches) one lane per pair:
 //                 (0) decode the 192-byte pair (bn256.go:120-164 G1.Unmarshal, :256-306 G2.Unmarshal):
 //                 coordinates < p, Montgomery encode, infinity detection, y^2 = x^3 + 3 on G1,
 //                 on-twist + subgroup membership on G2 (twist.go:47-63)  -> pair status + points;
@@ -51,22 +51,11 @@ template <class T>
 GSV_DI fp2 s2(const T& a) { return fp2_store(a); }
 GSV_DI fq fq_c(const uint32_t c[9]) { return fq_store(fq_const(c)); }
 
-// F_p^6 products of the F_p^12 routines: inline, or (BN_FP6_OOL) one out-of-line copy per operand
-// type pair, operands by pointer — a third of the code of an inlined F_p^12 product in the I-cache
-#ifndef BN_FP6_OOL
-#define BN_FP6_OOL 0
-#endif
-template <class A, class B, class R>
-static BN_NI void fp6_mul_ool(R* e, const fp6t<A>* a, const fp6t<B>* b) { *e = fp6_mul(*a, *b); }
+// F_p^6 products of the F_p^12 routines (inline; one out-of-line copy per operand type pair measured
+// no better, r02)
 template <class A, class B>
 GSV_DI auto fp6_mulx(const fp6t<A>& a, const fp6t<B>& b) {
-#if BN_FP6_OOL
-    decltype(fp6_mul(a, b)) r;
-    fp6_mul_ool(&r, &a, &b);
-    return r;
-#else
     return fp6_mul(a, b);
-#endif
 }
 
 // ---------------------------------------------------------------- F_p^12 (gfp12.go)
@@ -268,38 +257,7 @@ GSV_DI g2j g2_psi(const g2j& a) {
 GSV_DI bool g2_on_twist(const g2a& q) {
     return fp2_eq(fp2_sqr(q.y), fp2_add(fp2_mul(fp2_sqr(q.x), q.x), fp2_const(FQ_TWIST_B_X, FQ_TWIST_B_Y)));
 }
-// twist.go:47-63: y^2 == x^3 + 3/xi and Q in the order-r subgroup (the BN_SUB_FROB = 0 build)
-static BN_NI bool g2_in_subgroup(const g2a* pq) {
-    const g2a q = *pq;
-    if (!g2_on_twist(q)) return false;
-    // The reference decides membership with Order*Q == infinity (twist.go:60-62, 254-bit
-    // double-and-add).  We decide the same predicate with the endomorphism psi (the
-    // untwist-Frobenius-twist map the Miller loop already uses for Q1, optate.go:173-176):
-    //   [r]Q == O  <=>  [u+1]Q + psi([u]Q) + psi^2([u]Q) == psi^3([2u]Q)
-    // for every Q on E'(F_p^2) of BN254 (Dai-Lin-Zhao-Zhou, eprint 2022/348, sec. 3 and 5.1):
-    // a 63-bit multiplication instead of a 254-bit one.  Checked against the oracle's
-    // Order*Q on random points inside and outside G2 (tests/test_gpu_bn256.py).
-    g2j a{q.x, q.y, fp2_one(), fp2_one()};
-    // [u]Q, u = 4965661367192848881 (63 bits), NAF digits (24 nonzero instead of 28 set bits), mixed
-    // additions of the affine +-Q; inlined down to the F_p product: the running point stays in VGPRs
-    g2a mq{q.x, s2(fp2_neg(q.y))};
-    g2j uq = a;  // leading digit +1 at bit 62
-#pragma unroll 1
-    for (int i = 61; i >= 0; i--) {
-        uq = g2_double_i(uq);
-        bool pos = (U_NAF_POS >> i) & 1, neg = (U_NAF_NEG >> i) & 1;
-        if (pos || neg) uq = g2_add_mixed_i(uq, neg ? mq : q);
-    }
-    g2j p1 = g2_psi(uq);                                 // psi([u]Q)
-    g2j p2 = g2_psi(p1);                                 // psi^2([u]Q)
-    g2j lhs = g2_add_i(g2_add_i(g2_add_i(uq, a), p1), p2);  // [u+1]Q + psi([u]Q) + psi^2([u]Q)
-    g2j rhs = g2_psi(g2_psi(g2_psi(g2_double_i(uq))));   // psi^3([2u]Q)
-    rhs.y = s2(fp2_neg(rhs.y));
-    g2j d = g2_add_i(lhs, rhs);                          // lhs - rhs
-    return fp2_is_zero(d.z);
-}
-
-// Subgroup membership from the line chain's own final point (BN_SUB_FROB).  The lines of a pair leave
+// Subgroup membership from the line chain's own final point (r03).  The lines of a pair leave
 // r = [6u+2]Q + psi(Q) - psi^2(Q) (optate.go:122-210: the NAF doublings / additions, then the two
 // Frobenius additions), and for every Q on E'(F_p^2) of BN254
 //     [r]Q == O (twist.go:60-62)   <=>   r + psi^3(Q) == O.
@@ -312,7 +270,9 @@ static BN_NI bool g2_in_subgroup(const g2a* pq) {
 // case (r == +-q at an addition, a 2-torsion r at a doubling) only when they output Z = 0, which every
 // later step keeps at 0; that reads as "not in G2", and for Q in G2 no multiple the chain meets is
 // +-Q (6u+2 -+ p, 6u+2 + p -+ p^2 are nonzero mod r), so members never get there.  It replaces the
-// separate 63-bit psi test: no second G2 chain per pair.
+// separate 63-bit psi test of r02 (the ISA-level membership test of Dai-Lin-Zhao-Zhou, eprint 2022/348,
+// [u+1]Q + psi([u]Q) + psi^2([u]Q) == psi^3([2u]Q), on a second G2 chain per pair, in check waves beside
+// the lines): prepare 10.5 -> 6.5 ms per 65,536 checks (profiles/r03/ab_subfrob.txt).
 GSV_DI bool g2_frob_check(const g2j& r, const g2a& Q) {
     fp2 x = Q.x, y = Q.y;
 #pragma unroll
@@ -326,11 +286,6 @@ GSV_DI bool g2_frob_check(const g2j& r, const g2a& Q) {
 
 // ---------------------------------------------------------------- Miller loop (optate.go)
 struct line { fp2 a, b, c; };
-// 1: the line role's formulas ordered / fed for register pressure (pair_lines, line_double_i); the
-// field elements are the same
-#ifndef BN_LINES_LEAN
-#define BN_LINES_LEAN 1
-#endif
 // optate.go:3-50 (mixed addition r + p, p affine with t = 1; r2 = p.y^2)
 GSV_DI line line_add_i(g2j& r, const g2a& p, const g1a& q, const fp2& r2) {
     fp2 B = s2(fp2_mul(p.x, r.t));
@@ -363,8 +318,7 @@ GSV_DI line line_double_i(g2j& r, const g1a& q) {
     fp2 G = s2(fp2_sqr(E));
     line l;
     g2j o;
-#if BN_LINES_LEAN
-    // the same values in the order that ends each input's life earliest (r.x with l.a, r.y / r.z / B
+    // optate.go's values in the order that ends each input's life earliest (r.x with l.a, r.y / r.z / B
     // with o.z, r.t with l.b / l.c), against the line role's register pressure
     l.a = s2(fp2_sub(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.x, E)), A), G), fp2_mul_small<4>(B)));
     o.z = s2(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.y, r.z)), B), r.t));
@@ -373,15 +327,6 @@ GSV_DI line line_double_i(g2j& r, const g1a& q) {
     o.x = s2(fp2_sub(G, fp2_dbl(D)));
     o.y = s2(fp2_sub(fp2_mul(fp2_sub(D, o.x), E), fp2_mul_small<8>(C)));
     o.t = s2(fp2_sqr(o.z));
-#else
-    o.x = s2(fp2_sub(G, fp2_dbl(D)));
-    o.z = s2(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.y, r.z)), B), r.t));
-    o.y = s2(fp2_sub(fp2_mul(fp2_sub(D, o.x), E), fp2_mul_small<8>(C)));
-    o.t = s2(fp2_sqr(o.z));
-    l.b = s2(fp2_mul_fp(fp2_neg(fp2_dbl(fp2_mul(E, r.t))), q.x));
-    l.a = s2(fp2_sub(fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.x, E)), A), G), fp2_mul_small<4>(B)));
-    l.c = s2(fp2_mul_fp(fp2_dbl(fp2_mul(o.z, r.t)), q.y));
-#endif
     r = o;
     return l;
 }
@@ -482,7 +427,6 @@ enum : uint8_t { PS_OK = 0, PS_SKIP = 1, PS_BAD = 2 };
 GSV_DI g2j pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j, const g1a& P, const g2a& Q) {
     g2j r{Q.x, Q.y, fp2_one(), fp2_one()};
     int li = 0;
-#if BN_LINES_LEAN
     // -Q and r2 = Q.y^2 are formed at each addition step (27 of the 91) instead of living in VGPRs
     // through all of them: 36 fewer registers held against the line role's spills
 #pragma unroll 1
@@ -494,16 +438,6 @@ GSV_DI g2j pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j,
             line_store(lines, npairs, j, li++, line_add_i(r, q, P, s2(fp2_sqr(Q.y))));
         }
     }
-#else
-    fp2 r2 = s2(fp2_sqr(Q.y));
-    g2a mQ{Q.x, s2(fp2_neg(Q.y))};
-#pragma unroll 1
-    for (int i = 64; i > 0; i--) {
-        line_store(lines, npairs, j, li++, line_double_i(r, P));
-        uint64_t bit = 1ull << (i - 1);
-        if ((NAF_POS | NAF_NEG) & bit) line_store(lines, npairs, j, li++, line_add_i(r, (NAF_POS & bit) ? Q : mQ, P, r2));
-    }
-#endif
     // Q1 = pi(Q), -Q2 = -pi^2(Q) (optate.go:168-209)
     g2a q1{s2(fp2_mul(fp2_conj(Q.x), fp2_const(FQ_XI_P1_3_X, FQ_XI_P1_3_Y))),
            s2(fp2_mul(fp2_conj(Q.y), fp2_const(FQ_XI_P1_2_X, FQ_XI_P1_2_Y)))};
@@ -513,17 +447,10 @@ GSV_DI g2j pair_lines(uint32_t* __restrict__ lines, uint32_t npairs, uint32_t j,
     return r;
 }
 
-// 1: subgroup membership from the line chain (g2_frob_check), one lane per pair; 0: the separate check
-// role with the 63-bit psi test (A/B)
-#ifndef BN_SUB_FROB
-#define BN_SUB_FROB 1
-#endif
-// role 0 (checks) / role 1 (lines) of pair i.  With `luse` (the concurrent layout) the lines role also
-// writes whether the Miller loop uses the pair's lines: PS_OK for a decoded pair with neither point at
-// infinity, PS_SKIP otherwise; the curve / subgroup verdict (pstat) then arrives only for k_bn_final.
-GSV_DI void prepare_pair(bool role_lines, uint32_t i, const uint8_t* __restrict__ in, const uint64_t* __restrict__ pair_src,
-                         uint32_t npairs, uint8_t* __restrict__ pstat, uint32_t* __restrict__ lines,
-                         uint8_t* __restrict__ luse = nullptr) {
+// One lane does a whole pair: decode (bn256.go:120-164, 256-306), curve checks, the 91 lines, and
+// membership from the lines' final point (g2_frob_check).
+GSV_DI void prepare_pair(uint32_t i, const uint8_t* __restrict__ in, const uint64_t* __restrict__ pair_src,
+                         uint32_t npairs, uint8_t* __restrict__ pstat, uint32_t* __restrict__ lines) {
     const uint8_t* s = in + pair_src[i];
     g1a P;
     g2a Q;
@@ -535,73 +462,23 @@ GSV_DI void prepare_pair(bool role_lines, uint32_t i, const uint8_t* __restrict_
     ok = fp_unmarshal(Q.y.y, s + 160) && ok;
     bool inf1 = fq_is_zero(P.x) && fq_is_zero(P.y);
     bool inf2 = fp2_is_zero(Q.x) && fp2_is_zero(Q.y);
-#if BN_SUB_FROB
-    // one lane does the whole pair: curve checks, lines, and membership from the lines' final point
-    (void)role_lines;
-    (void)luse;
     if (ok && !inf1)  // curve.go:39-52: y^2 == x^3 + 3
         ok = fq_eq(fq_mul(P.y, P.y), fq_add(fq_mul(fq_mul(P.x, P.x), P.x), fq_const(FQ_THREE)));
     if (ok && !inf2) ok = g2_on_twist(Q);
     g2j r = pair_lines(lines, npairs, i, P, Q);
     if (ok && !inf2) ok = g2_frob_check(r, Q);
     pstat[i] = !ok ? PS_BAD : (inf1 || inf2) ? PS_SKIP : PS_OK;
-    return;
-#endif
-    if (role_lines) {
-        if (luse) luse[i] = ok && !inf1 && !inf2 ? PS_OK : PS_SKIP;
-        pair_lines(lines, npairs, i, P, Q);
-        return;
-    }
-    if (ok && !inf1)  // curve.go:39-52: y^2 == x^3 + 3
-        ok = fq_eq(fq_mul(P.y, P.y), fq_add(fq_mul(fq_mul(P.x, P.x), P.x), fq_const(FQ_THREE)));
-    if (ok && !inf2) ok = g2_in_subgroup(&Q);
-    pstat[i] = !ok ? PS_BAD : (inf1 || inf2) ? PS_SKIP : PS_OK;
 }
 
-// Blocks [0, nb) are role 0 (checks), blocks [nb, 2 nb) role 1 (lines) of the same 64 pairs: the
-// roles are whole waves, so they run side by side on different SIMDs without divergence.
-// BN_PREP_WAVES waves per SIMD (a register budget of 512 / BN_PREP_WAVES): simple VALU ops issue at
-// twice the rate with a second wave (profiles/r01_microbench_lat.txt), against the spills of a
-// 256-register budget.
-#ifndef BN_PREP_WAVES
-#define BN_PREP_WAVES 2
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVES))) void k_bn_prepare(const uint8_t* __restrict__ in,
-                                                   const uint64_t* __restrict__ pair_src,
-                                                   uint32_t npairs, uint8_t* __restrict__ pstat,
-                                                   uint32_t* __restrict__ lines /* [91 * 54 words][npairs] */) {
-#if BN_SUB_FROB
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // one role: grid of (npairs + 63) / 64 blocks
-    if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, pstat, lines);
-#else
-    uint32_t nb = (npairs + 63) / 64;
-    bool role_lines = blockIdx.x >= nb;
-    uint32_t i = (role_lines ? blockIdx.x - nb : blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= npairs) return;
-    prepare_pair(role_lines, i, in, pair_src, npairs, pstat, lines);
-#endif
-}
-// BN_PREP_SPLIT: the two roles as separate kernels, each with its own register budget (A/B)
-#ifndef BN_PREP_SPLIT
-#define BN_PREP_SPLIT 0
-#endif
-#ifndef BN_LINES_WAVES
-#define BN_LINES_WAVES 1
-#endif
-#if !BN_SUB_FROB
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_PREP_WAVES))) void k_bn_check(const uint8_t* __restrict__ in,
-                                                   const uint64_t* __restrict__ pair_src,
-                                                   uint32_t npairs, uint8_t* __restrict__ pstat) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < npairs) prepare_pair(false, i, in, pair_src, npairs, pstat, nullptr);
-}
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_LINES_WAVES))) void k_bn_lines(const uint8_t* __restrict__ in,
+// k_bn_lines: one wave per SIMD (no spills).  A two-wave budget of the same code (k_bn_prepare through
+// r05) spilled 696 B per lane and took the same time at 65,536 checks (7.26 vs 7.27 ms, r04); large
+// batches take k_bn_lines_w2 below.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_bn_lines(const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ pair_src,
                                                    uint32_t npairs, uint32_t* __restrict__ lines,
-                                                   uint8_t* __restrict__ luse, uint8_t* __restrict__ pstat) {
+                                                   uint8_t* __restrict__ pstat) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < npairs) prepare_pair(true, i, in, pair_src, npairs, pstat, lines, luse);
+    if (i < npairs) prepare_pair(i, in, pair_src, npairs, pstat, lines);
 }
 
 // ---- the lines role at TWO waves per SIMD (k_bn_lines_w2).  A configs[4] batch has 4 x 65,536 pairs:
@@ -609,7 +486,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BN_LINES_WAV
 // lines need no extra split to fill a second wave.  k_bn_lines holds 256 + 125 registers; what moves
 // here: P and Q wait in LDS ([54 words][64 lanes], 13.8 KB per wave) and are read where a line needs
 // them, and each line coefficient is stored to HBM as soon as it is computed instead of after the step.
-// The formulas and their order are line_double_i / line_add_i's (BN_LINES_LEAN), so the lines are the
+// The formulas and their order are line_double_i / line_add_i's, so the lines are the
 // same F_p^2 values.
 #define LW2_SEQ __builtin_amdgcn_sched_barrier(0)
 GSV_DI void lw2_put(uint32_t* l, int j, const fq& v) {
@@ -673,12 +550,11 @@ GSV_DI void line_add_w2(g2j& r, const g2a& p, const fp2& r2, const uint32_t* l, 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_bn_lines_w2(const uint8_t* __restrict__ in,
                                                    const uint64_t* __restrict__ pair_src,
                                                    uint32_t npairs, uint32_t* __restrict__ lines,
-                                                   uint8_t* __restrict__ luse, uint8_t* __restrict__ pstat) {
+                                                   uint8_t* __restrict__ pstat) {
     __shared__ uint32_t lds[54 * 64];
     uint32_t* l = lds + threadIdx.x;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npairs) return;
-    (void)luse;
     bool ok, inf1, inf2;
     {
         const uint8_t* s = in + pair_src[i];
@@ -746,9 +622,7 @@ enum : uint8_t { CS_OK = 0, CS_BAD = 1, CS_ONE = 2 };  // CS_ONE: no finite pair
 // A lane runs the loop over a group of <= k of its check's pairs (k = 4 covers a whole 4-pair check;
 // smaller k when the batch is too small to give every SIMD work — the host's choice), and k_bn_final
 // multiplies a check's lane values: the same exact product, so the same verdict.
-#ifndef BN_MILLER_WAVES
-#define BN_MILLER_WAVES 1
-#endif
+constexpr int BN_MILLER_WAVES = 1;  // the Miller kernels' register budget: one wave per SIMD (256 + 256)
 // (Through r04 a BN_MILLER_PREFETCH form loaded each line one multiplication ahead; the held line cost
 // 177 AGPRs and ~650 accumulator moves, and without it the Miller kernel ran 8.75 -> 8.30 ms at 65,536
 // checks, profiles/r04/ab/pf_prefetch{1,0}_*.json.  Unused since, removed in r05.)
@@ -1263,13 +1137,11 @@ enum : uint8_t {
     FE_LDFV,   // A = the next Miller-lane value of the check (prologue; not in the program)
     FE_CSQR_LDA,  // X = X^2 while A = ws[slot] is fetched (the loads issue before the squaring)
 };
-// BN_FE_W4 = 1: the exponentiations by u use width-4 signed digits of u (13 products below the leading
-// digit instead of the NAF's 23, plus 3 for the odd powers a^3, a^5, a^7).  The odd powers go to
-// workspace slots 4..7; each digit's power is fetched into A during the squaring after the previous
-// product, so its load latency hides under that squaring.  0: the NAF (A = a throughout).
-#ifndef BN_FE_W4
-#define BN_FE_W4 1
-#endif
+// The exponentiations by u use width-4 signed digits of u (13 products below the leading digit instead
+// of the NAF's 23, plus 3 for the odd powers a^3, a^5, a^7).  The odd powers go to workspace slots 4..7;
+// each digit's power is fetched into A during the squaring after the previous product, so its load
+// latency hides under that squaring.  (The NAF form, A = a throughout, moves ~0.45 instead of 1.76 GB
+// per 65,536-check launch at 8-14 % more time, r04.)
 // width-4 digits of u below bit 62 (u = 2^62 + sum d_i 2^i, constants.go:17): bit i of U_W4_NZ set
 // where d_i != 0, of U_W4_NEG where d_i < 0; (|d_i| - 1) / 2 = U_W4_I0 bit + 2 U_W4_I1 bit
 constexpr uint64_t U_W4_NZ = 0x108844442110211ULL, U_W4_NEG = 0x8004400010010ULL;
@@ -1287,7 +1159,6 @@ struct FeBuild {
     // X = A^u (gfp12.go:113-127 on the NAF of u, constants.go:17; a^-1 = conj(a) in the cyclotomic
     // subgroup); A unchanged
     constexpr void exp_u() {
-#if BN_FE_W4
         e(FE_AX), e(FE_STX, FE_T0), e(FE_CSQR), e(FE_XA), e(FE_LDX, FE_T0);  // A = a^2, X = a
         for (int k = 1; k < 4; k++) e(FE_MUL), e(FE_STX, FE_T0 + k);         // a^3, a^5, a^7
         e(FE_LDX, FE_T0);                                                     // the leading digit
@@ -1311,14 +1182,6 @@ struct FeBuild {
             }
         }
         e(FE_LDA, FE_T0);  // A = a again
-#else
-        e(FE_AX);  // the leading digit (bit 62)
-        for (int i = 61; i >= 0; i--) {
-            e(FE_CSQR);
-            if ((U_NAF_POS >> i) & 1) e(FE_MUL);
-            if ((U_NAF_NEG >> i) & 1) e(FE_MULC);
-        }
-#endif
     }
     constexpr FeProg build() {
         // easy part: X = in
@@ -1592,16 +1455,9 @@ GSV_DI fp12 final_exp_run(fp12 X, const FinalArgs& fa, uint32_t* lds_base, uint3
 
 // cbad[c] != 0: the check's input length is not a multiple of 192 (errBadPairingInput,
 // core/vm/contracts.go:336-338); it has no pairs
-// PairBad (concurrent layout): the check kernel's per-pair verdicts, read here because the Miller
-// loop ran on the lines role's PS_OK / PS_SKIP alone
-struct PairBad {
-    const uint32_t* lane_first;
-    const uint32_t* pidx;
-    const uint8_t* pstat;  // nullptr: the Miller loop already saw pstat (lstat CS_BAD)
-};
 // the verdict is written by the lane of role 0
 template <bool COOP>
-GSV_DI void final_check(const FinalArgs& fa, const PairBad& pb, uint32_t* lds_base) {
+GSV_DI void final_check(const FinalArgs& fa, uint32_t* lds_base) {
     const FeLane<COOP> ln;
     if (COOP && ln.t() >= FINAL3_PER_WAVE) return;
     uint32_t c = ln.check();
@@ -1609,8 +1465,6 @@ GSV_DI void final_check(const FinalArgs& fa, const PairBad& pb, uint32_t* lds_ba
     uint32_t l0 = fa.check_lane[c], l1 = fa.check_lane[c + 1];
     bool bad = fa.cbad[c] != 0;
     for (uint32_t l = l0; l < l1; l++) bad = bad || fa.lstat[l] == CS_BAD;
-    if (pb.pstat)
-        for (uint32_t q = pb.lane_first[l0]; q < pb.lane_first[l1]; q++) bad = bad || pb.pstat[pb.pidx[q]] == PS_BAD;
     if (bad) {
         if (ln.role() == 0) fa.verdict[c] = GSV_PAIRING_BAD_INPUT;
         return;
@@ -1622,13 +1476,13 @@ GSV_DI void final_check(const FinalArgs& fa, const PairBad& pb, uint32_t* lds_ba
     if (ln.role() == 0) fa.verdict[c] = fp12_is_one(r) ? GSV_PAIRING_TRUE : GSV_PAIRING_FALSE;
 }
 
-__global__ __launch_bounds__(64) void k_bn_final(FinalArgs fa, PairBad pb) {
+__global__ __launch_bounds__(64) void k_bn_final(FinalArgs fa) {
     __shared__ uint32_t lds[(FE_LDS_V0 + 48) * 64];  // per lane: the machine's operand A, a product's v0
-    final_check<false>(fa, pb, lds);
+    final_check<false>(fa, lds);
 }
-__global__ __launch_bounds__(64) void k_bn_final3(FinalArgs fa, PairBad pb) {
+__global__ __launch_bounds__(64) void k_bn_final3(FinalArgs fa) {
     __shared__ uint32_t lds[108 * 64];
-    final_check<true>(fa, pb, lds);
+    final_check<true>(fa, lds);
 }
 
 
@@ -1818,7 +1672,6 @@ __global__ __launch_bounds__(64) void k_bn_synth(uint64_t seed, uint32_t nchecks
 
 }  // namespace bn
 
-bool bn256_layout_forks() { return !BN_SUB_FROB; }
 
 hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st) {
     if (nchecks == 0) return hipSuccess;
@@ -1832,57 +1685,17 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
                                 uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
                                 uint32_t* d_fws, uint32_t maxl, uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
-                                void (*timer_end)(void*, int), void* tctx, const BnConcurrent* conc) {
-    // GSV_BN_LAYOUT_CONC: the curve / subgroup checks run on a side stream beside the lines, the Miller
-    // loop (on the lines role's PS_OK / PS_SKIP) and join before the final exponentiation, which reads
-    // their verdicts; the lines kernel has a one-wave register budget (no spills).  For batches that
-    // leave SIMDs idle: the check waves fill them.
-    // BN_SUB_FROB: no check role (membership comes from the lines), so GSV_BN_LAYOUT_CONC only selects
-    // the one-wave-budget lines kernel; nothing forks.
-    const bool cc = !BN_SUB_FROB && (layout & GSV_BN_LAYOUT_CONC) && conc && npairs;
-    bn::PairBad pb{d_lane_first, d_pidx, cc ? d_pstat : nullptr};
-    const uint8_t* d_use = cc ? conc->d_luse : d_pstat;
-    if (BN_SUB_FROB && npairs) {
+                                void (*timer_end)(void*, int), void* tctx) {
+    // the pairs: decode, curve checks, lines, G2 membership (k_bn_lines, or its two-wave form LINESW2)
+    const uint8_t* d_use = d_pstat;
+    if (npairs) {
         if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        if ((layout & GSV_BN_LAYOUT_CONC) && (layout & GSV_BN_LAYOUT_LINESW2))
+        if (layout & GSV_BN_LAYOUT_LINESW2)
             hipLaunchKernelGGL(bn::k_bn_lines_w2, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                               d_lines, (uint8_t*)nullptr, d_pstat);
-        else if (layout & GSV_BN_LAYOUT_CONC)
-            hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                               d_lines, (uint8_t*)nullptr, d_pstat);
+                               d_lines, d_pstat);
         else
-            hipLaunchKernelGGL(bn::k_bn_prepare, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                               d_pstat, d_lines);
-        if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    } else if (cc) {
-        if (hipEventRecord(conc->fork, st) != hipSuccess || hipStreamWaitEvent(conc->side, conc->fork, 0) != hipSuccess)
-            return hipErrorUnknown;
-#if !BN_SUB_FROB
-        hipLaunchKernelGGL(bn::k_bn_check, dim3((npairs + 63) / 64), dim3(64), 0, conc->side, d_in, d_pair_src, npairs,
-                           d_pstat);
-#endif
-        if (hipEventRecord(conc->join, conc->side) != hipSuccess) return hipErrorUnknown;
-        if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs, d_lines,
-                           conc->d_luse, (uint8_t*)nullptr);
-        if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    } else if (npairs) {
-        if (timer_begin) timer_begin(tctx, GSV_K_BN_PREPARE);
-        if (!BN_SUB_FROB && BN_PREP_SPLIT) {
-#if !BN_SUB_FROB
-            hipLaunchKernelGGL(bn::k_bn_check, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                               d_pstat);
             hipLaunchKernelGGL(bn::k_bn_lines, dim3((npairs + 63) / 64), dim3(64), 0, st, d_in, d_pair_src, npairs,
-                               d_lines, (uint8_t*)nullptr, (uint8_t*)nullptr);
-#endif
-        } else {
-            hipLaunchKernelGGL(bn::k_bn_prepare, dim3(2 * ((npairs + 63) / 64)), dim3(64), 0, st, d_in, d_pair_src,
-                               npairs, d_pstat, d_lines);
-        }
+                               d_lines, d_pstat);
         if (timer_end) timer_end(tctx, GSV_K_BN_PREPARE);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -1907,17 +1720,14 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
         if (timer_end) timer_end(tctx, GSV_K_PAIRING);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        if (cc && hipStreamWaitEvent(st, conc->join, 0) != hipSuccess) return hipErrorUnknown;
         if (timer_begin) timer_begin(tctx, GSV_K_BN_FINAL);
         bn::FinalArgs fa{d_check_lane, nchecks, d_cbad, d_lstat, d_fv, nlanes, d_verdict, d_fws, maxl};
         if (layout & GSV_BN_LAYOUT_FINAL3)
             hipLaunchKernelGGL(bn::k_bn_final3, dim3((nchecks + bn::FINAL3_PER_WAVE - 1) / bn::FINAL3_PER_WAVE),
-                               dim3(64), 0, st, fa, pb);
+                               dim3(64), 0, st, fa);
         else
-            hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, fa, pb);
+            hipLaunchKernelGGL(bn::k_bn_final, dim3((nchecks + 63) / 64), dim3(64), 0, st, fa);
         if (timer_end) timer_end(tctx, GSV_K_BN_FINAL);
-    } else if (cc && hipStreamWaitEvent(st, conc->join, 0) != hipSuccess) {
-        return hipErrorUnknown;
     }
     return hipGetLastError();
 }

@@ -54,10 +54,7 @@ struct PChild {
 
 constexpr int MSG_STRIDE = 544;  // bytes per message buffer (532 max + padding to the 4th block end);
                                  // an HFULL node's buffer holds its 16 children's raw hashes (512 B)
-#ifndef GSV_TOP_MAX_HFULL
-#define GSV_TOP_MAX_HFULL 1024
-#endif
-constexpr int TOP_MAX_HFULL = GSV_TOP_MAX_HFULL;  // fused-top eligibility per height (per body)
+constexpr int TOP_MAX_HFULL = 1024;  // fused-top eligibility per height (per body)
 constexpr int TOP_MAX_GEN = 64;
 constexpr int TOP_MAX_H = 24;
 constexpr int REF_STRIDE = 48;   // bytes per ref slot: [0] = length, [8..41) = ref bytes

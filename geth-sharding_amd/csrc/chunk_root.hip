@@ -372,18 +372,12 @@ GSV_DI void emit_hash(const PNode& nd, const BodyBatch& bb, uint32_t body, const
 
 // ---------------------------------------------------------------- BOTTOM: 16 leaf children
 // leaf j = [0x20, rlp(b)]: b == 0 -> c3 20 81 80; b < 128 -> c2 20 b; else c4 20 82 81 b
-#ifndef GSV_BOT_PREZERO
-#define GSV_BOT_PREZERO 1
-#endif
 constexpr int BOT_BLOCK = 256;
 // a lane's message buffer stride in LDS (bytes, a multiple of 8, >= 88): 96 = 24 words put the 64
 // lanes of a wave on 4 of the 32 banks (8-way conflicts for the 64-bit accesses); 88 (22 words) spreads
 // them over 16.  r05: bottom level 0.80 vs 0.82 ms, configs[2] equal within noise
-// (profiles/r05/ab/bottom_lds_stride.txt).  GSV_BOT_BUF overrides (A/B).
-#ifndef GSV_BOT_BUF
-#define GSV_BOT_BUF 88
-#endif
-constexpr int BOT_BUF = GSV_BOT_BUF;
+// (profiles/r05/ab/bottom_lds_stride.txt).
+constexpr int BOT_BUF = 88;
 static_assert(BOT_BUF % 8 == 0 && BOT_BUF >= 88, "the 88-byte window, 8-byte aligned");
 
 // m: this lane's BOT_BUF-byte LDS buffer (8-byte aligned)
@@ -402,7 +396,6 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
     uint32_t payload = 1;  // trailing empty value slot 0x80
 #pragma unroll
     for (int j = 0; j < 16; j++) payload += v[j] == 0 ? 4u : v[j] < 128 ? 3u : 5u;
-#if GSV_BOT_PREZERO
     // the 88-byte window zeroed by eleven 64-bit stores up front (no per-byte tail loop), the sponge's
     // 0x01 pad byte stored after the message instead of XOR-ed into the loaded word by lane compares
     {
@@ -410,7 +403,6 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
 #pragma unroll
         for (int k = 0; k < 11; k++) mz[k] = 0;
     }
-#endif
     uint32_t o = 0;
     if (payload < 56) {
         m[o++] = (uint8_t)(0xc0 + payload);
@@ -433,94 +425,11 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
         }
     }
     m[o++] = 0x80;
-#if GSV_BOT_PREZERO
     m[o] = 0x01;  // single block: len <= 83 < 136
     uint64_t a[25];
     const uint64_t* q = (const uint64_t*)m;
 #pragma unroll
     for (int k = 0; k < 11; k++) a[k] = q[k];
-#pragma unroll
-    for (int k = 11; k < 25; k++) a[k] = 0;
-#else
-    // zero the rest of the 88-byte window, then pad (single block: len <= 83 < 136)
-    for (uint32_t k = o; k < 88; k++) m[k] = 0;
-    uint64_t a[25];
-    const uint64_t* q = (const uint64_t*)m;
-#pragma unroll
-    for (int k = 0; k < 11; k++) a[k] = q[k];
-#pragma unroll
-    for (int k = 11; k < 25; k++) a[k] = 0;
-    // 0x01 at byte o (o <= 83 -> lane <= 10)
-    uint32_t lane = o >> 3;
-#pragma unroll
-    for (int k = 0; k < 11; k++)
-        if ((uint32_t)k == lane) a[k] ^= 0x01ull << (8 * (o & 7u));
-#endif
-    a[16] ^= 0x8000000000000000ULL;
-    keccakf(a);
-    uint32_t h[8];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        h[2 * k] = (uint32_t)a[k];
-        h[2 * k + 1] = (uint32_t)(a[k] >> 32);
-    }
-    emit_hash(nd, bb, body, h);
-}
-
-// Branch-free form (GSV_BOT_OR, A/B): each child's 3-5 bytes are one 40-bit value (bytes little-endian)
-// OR-ed into two aligned 32-bit words of a prezeroed [word pair][lane] LDS buffer at its running byte
-// offset (ds_or_b32), instead of 3-5 byte stores in a three-way branch that diverges on random bytes.
-#ifndef GSV_BOT_OR
-#define GSV_BOT_OR 0
-#endif
-GSV_DI void lds_or(uint32_t* p, uint32_t v) { __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-// base: the workgroup's buffer, word pair k of lane t at base[k * BOT_BLOCK + t]
-GSV_DI void do_bottom_or(const PNode& nd, const BodyBatch& bb, uint32_t body, uint64_t* base, uint32_t t) {
-    const uint8_t* src = bb.bodies + bb.body_off[body] + nd.first_i;
-    uint8_t v[16];
-    if ((((uintptr_t)src) & 15u) == 0) {
-        uint4 w = *(const uint4*)src;
-        uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int j = 0; j < 16; j++) v[j] = (uint8_t)(ws[j >> 2] >> (8 * (j & 3)));
-    } else {
-#pragma unroll
-        for (int j = 0; j < 16; j++) v[j] = src[j];
-    }
-    uint32_t payload = 1;  // trailing empty value slot 0x80
-#pragma unroll
-    for (int j = 0; j < 16; j++) payload += v[j] == 0 ? 4u : v[j] < 128 ? 3u : 5u;
-    uint64_t* m64 = base + t;
-#pragma unroll
-    for (int k = 0; k < 11; k++) m64[k * BOT_BLOCK] = 0;
-    uint32_t* m32 = (uint32_t*)m64;
-    auto wp = [&](uint32_t w) { return m32 + (w >> 1) * (2u * BOT_BLOCK) + (w & 1u); };
-    uint32_t o;
-    if (payload < 56) {
-        lds_or(wp(0), 0xc0u + payload);
-        o = 1;
-    } else {
-        lds_or(wp(0), 0xf8u | (payload << 8));
-        o = 2;
-    }
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint32_t b = v[j];
-        const bool z = b == 0, hi = b >= 128;
-        const uint32_t lo = hi ? 0x818220c4u : z ? 0x808120c3u : (0x20c2u | (b << 16));
-        const uint64_t e = (((uint64_t)(hi ? b : 0u) << 32) | lo) << ((o & 3u) * 8u);
-        lds_or(wp(o >> 2), (uint32_t)e);
-        lds_or(wp((o >> 2) + 1u), (uint32_t)(e >> 32));
-        o += hi ? 5u : z ? 4u : 3u;
-    }
-    {  // the empty value slot 0x80, then the sponge's 0x01 pad (single block: length <= 83 < 136)
-        const uint64_t e = (uint64_t)0x0180u << ((o & 3u) * 8u);
-        lds_or(wp(o >> 2), (uint32_t)e);
-        lds_or(wp((o >> 2) + 1u), (uint32_t)(e >> 32));
-    }
-    uint64_t a[25];
-#pragma unroll
-    for (int k = 0; k < 11; k++) a[k] = m64[k * BOT_BLOCK];
 #pragma unroll
     for (int k = 11; k < 25; k++) a[k] = 0;
     a[16] ^= 0x8000000000000000ULL;
@@ -579,13 +488,6 @@ GSV_DI void hf_load(HfWin<B>& W, const uint4* __restrict__ Hq) {
         W.w[8 * s + 4] = b.x; W.w[8 * s + 5] = b.y; W.w[8 * s + 6] = b.z; W.w[8 * s + 7] = b.w;
     }
 }
-// the loaded words are "used" here, so the loads stay where they were issued (before the permutation
-// they overlap) instead of being sunk to their real use
-template <int B>
-GSV_DI void hf_pin(HfWin<B>& W) {
-#pragma unroll
-    for (int k = 0; k < HfWin<B>::ns * 8; k++) asm volatile("" : "+v"(W.w[k]));
-}
 template <int B>
 GSV_DI void hf_absorb_block(uint32_t al[25], uint32_t ah[25], const HfWin<B>& W) {
     hf_absorb<B>(al, ah, W.w, std::make_integer_sequence<int, 17>{});
@@ -594,15 +496,12 @@ GSV_DI void hf_absorb_block(uint32_t al[25], uint32_t ah[25], const HfWin<B>& W)
         ah[16] ^= 0x80000000u;
     }
 }
-#ifndef GSV_HF_PREFETCH
-#define GSV_HF_PREFETCH 0
-#endif
 // Keccak-256 of the full branch f9 02 11 | (a0 || H_0) ... (a0 || H_15) | 80 (532 bytes, 4 blocks).
 // Every byte's source is a compile-time function of its offset (templates above), so each 32-bit
 // message word is a v_perm / shift of at most two child-hash words held in registers — no message
-// buffer.  GSV_HF_PREFETCH = 1 (A/B, r05): block B + 1's child-hash words are loaded before block B's
-// permutation; measured slower (configs[2] 100.0 vs 101.3 GB/s: the held words raise the level kernel
-// to 129 VGPRs, three waves per SIMD; profiles/r05/ab/hfull_prefetch.txt), so off.
+// buffer.  Block B + 1's child-hash words are loaded after block B's permutation: loading them before
+// measured slower (r05: configs[2] 100.0 vs 101.3 GB/s, the held words raise the level kernel to 129
+// VGPRs, three waves per SIMD; profiles/r05/ab/hfull_prefetch.txt).
 GSV_DI void hash_hfull(uint32_t h[8], const uint32_t* __restrict__ H) {
     uint32_t al[25], ah[25];
 #pragma unroll
@@ -614,19 +513,6 @@ GSV_DI void hash_hfull(uint32_t h[8], const uint32_t* __restrict__ H) {
     HfWin<3> w3;
     hf_load(w0, Hq);
     hf_absorb_block(al, ah, w0);
-#if GSV_HF_PREFETCH
-    hf_load(w1, Hq);
-    hf_pin(w1);
-    keccakf_split(al, ah);
-    hf_absorb_block(al, ah, w1);
-    hf_load(w2, Hq);
-    hf_pin(w2);
-    keccakf_split(al, ah);
-    hf_absorb_block(al, ah, w2);
-    hf_load(w3, Hq);
-    hf_pin(w3);
-    keccakf_split(al, ah);
-#else
     keccakf_split(al, ah);
     hf_load(w1, Hq);
     hf_absorb_block(al, ah, w1);
@@ -635,7 +521,6 @@ GSV_DI void hash_hfull(uint32_t h[8], const uint32_t* __restrict__ H) {
     hf_absorb_block(al, ah, w2);
     keccakf_split(al, ah);
     hf_load(w3, Hq);
-#endif
     hf_absorb_block(al, ah, w3);
     keccakf_split(al, ah);
 #pragma unroll
@@ -913,18 +798,10 @@ struct LevelLaunch {
     uint32_t gen_blocks;
     int gen_lane;  // 1: one generic node per lane (gen_blocks of 256 lanes), 0: one per wave
 };
-// GSV_LEVEL_WAVES: register budget of the level kernels (waves per SIMD; 0 = the compiler's choice,
-// 100 VGPRs = four waves)
-#ifndef GSV_LEVEL_WAVES
-#define GSV_LEVEL_WAVES 0
-#endif
-#if GSV_LEVEL_WAVES
-#define GSV_LEVEL_ATTR __attribute__((amdgpu_waves_per_eu(GSV_LEVEL_WAVES, GSV_LEVEL_WAVES)))
-#else
-#define GSV_LEVEL_ATTR
-#endif
+// The level kernels keep the compiler's register budget (four waves per SIMD); five waves (96 VGPRs)
+// measured within +-2 % (r03, r05: profiles/r05/ab/chunk_levels5_unroll2.txt).
 template <bool BOT>
-__global__ __launch_bounds__(256) GSV_LEVEL_ATTR void k_chunk_level(const PNode* __restrict__ nodes,
+__global__ __launch_bounds__(256) void k_chunk_level(const PNode* __restrict__ nodes,
                                                      const PChild* __restrict__ children, LevelLaunch L,
                                                      BodyBatch bb) {
     __shared__ uint64_t sbuf[(BOT ? 256 * BOT_BUF : 8 * MSG_STRIDE) / 8];
@@ -948,48 +825,24 @@ __global__ __launch_bounds__(256) GSV_LEVEL_ATTR void k_chunk_level(const PNode*
     if (t >= (uint64_t)L.nn * bb.nbodies) return;
     uint32_t body = (uint32_t)(t / (uint64_t)L.nn);
     const PNode nd = nodes[L.n0 + (int)(t % (uint64_t)L.nn)];
-#if GSV_BOT_OR
-    if constexpr (BOT) do_bottom_or(nd, bb, body, sbuf, threadIdx.x);
-#else
     if constexpr (BOT) do_bottom(nd, bb, body, (uint8_t*)sbuf + threadIdx.x * BOT_BUF);
-#endif
     else do_hfull(nd, bb, body);
 }
 
 // ---------------------------------------------------------------- fused top of the trie
-#ifndef GSV_TOP_PRIO_DEFAULT
-#define GSV_TOP_PRIO_DEFAULT 0
-#endif
 struct TopLevels {
     int h0, h1;  // heights h0..h1 (inclusive), index h - 1 below
     int hb[TOP_MAX_H], he[TOP_MAX_H], gb[TOP_MAX_H], ge[TOP_MAX_H];
     uint32_t gen_lane;  // bit h - 1: that height's generic nodes one per lane (throughput form)
-    int prio;           // nonzero: the top's waves run at the highest wave priority (s_setprio 3)
 };
 // The fused top is a short dependent chain (~17 permutations from height 3 to the root) that usually
 // runs BESIDE bulk work: the next batch's bottom level (pipelined chunk roots) or k_notary_tx (the
-// notary forks its chunk roots onto a side stream).  At equal priority the SQ's arbiter shares each
-// SIMD's issue slots among all resident waves, so the top's chain advances at a fraction of its speed
-// and its workgroups hold their CUs' wave slots and LDS for the whole overlap.  At priority 3 its
-// waves issue first: the chain finishes in about its solo time and hands the slots back.
-// Measured within noise (r04: configs[2] 91.7 vs 91.8 GB/s, the notary leg 9,844 vs 9,843 shards/s,
-// 13 / 100 shards per step unchanged), so it is off by default; GSV_TOP_PRIO = 0 / 1 overrides.
-inline int top_prio() {
-    static int p = [] {
-        const char* e = getenv("GSV_TOP_PRIO");
-        return e ? atoi(e) : GSV_TOP_PRIO_DEFAULT;
-    }();
-    return p;
-}
+// notary forks its chunk roots onto a side stream).  Running its waves at the highest wave priority
+// (s_setprio 3) measured within noise (r04: configs[2] 91.7 vs 91.8 GB/s, the notary leg 9,844 vs 9,843
+// shards/s; profiles/r04/ab/notary_sweep_top_prio{0,1}.txt), so they run at the default priority.
 constexpr uint32_t TOP_MAX_BODIES = 256;  // one fused-top workgroup per CU at most
-#ifndef GSV_TOP_HFULL_THREADS
-#define GSV_TOP_HFULL_THREADS 256
-#endif
-constexpr int TOP_HFULL_THREADS = GSV_TOP_HFULL_THREADS;  // waves 0-3: HFULL nodes, one per lane
-#ifndef GSV_TOP_GEN_WAVES
-#define GSV_TOP_GEN_WAVES 2
-#endif
-constexpr int TOP_GEN_WAVES = GSV_TOP_GEN_WAVES;  // waves 4..: generic nodes, one per wave (never behind HFULL work)
+constexpr int TOP_HFULL_THREADS = 256;    // waves 0-3: HFULL nodes, one per lane (64 / 128: within +-2 %, r03)
+constexpr int TOP_GEN_WAVES = 2;          // waves 4..: generic nodes, one per wave (never behind HFULL work)
 constexpr int TOP_BLOCK = TOP_HFULL_THREADS + 64 * TOP_GEN_WAVES;
 
 // one workgroup per body, a barrier between heights (children's hashes are in the CU's L1/L2).
@@ -999,28 +852,15 @@ constexpr int TOP_BLOCK = TOP_HFULL_THREADS + 64 * TOP_GEN_WAVES;
 constexpr int TOP_GROUPS = TOP_BLOCK / 32;
 constexpr int TOP_COOP_MAX = TOP_GROUPS;  // nodes per height up to which every node is group-hashed (one round)
 
-// register budget of the fused top (GSV_TOP_WAVES waves per SIMD, 0 = the compiler's choice, 178 VGPRs):
-// its waves sit beside the next batch's bottom level, and a smaller allocation leaves that level more
-// of each SIMD's register file (A/B)
-#ifndef GSV_TOP_WAVES
-#define GSV_TOP_WAVES 0
-#endif
-#if GSV_TOP_WAVES
-#define GSV_TOP_ATTR __attribute__((amdgpu_waves_per_eu(GSV_TOP_WAVES)))
-#else
-#define GSV_TOP_ATTR
-#endif
-__global__ __launch_bounds__(TOP_BLOCK) GSV_TOP_ATTR void k_chunk_top(const PNode* __restrict__ nodes,
+// The fused top keeps the compiler's register budget (a smaller one, leaving the next batch's bottom
+// level more of each SIMD's register file, measured null: profiles/r05/ab/top_register_budget.txt).
+__global__ __launch_bounds__(TOP_BLOCK) void k_chunk_top(const PNode* __restrict__ nodes,
                                                          const PChild* __restrict__ children, TopLevels tl,
                                                          BodyBatch bb) {
     __shared__ uint64_t gbuf[TOP_GROUPS * MSG_STRIDE / 8];
-    if (tl.prio) __builtin_amdgcn_s_setprio(3);
     uint32_t body = blockIdx.x;
     int tid = threadIdx.x, grp = tid >> 5;
     uint8_t* m = (uint8_t*)gbuf + grp * MSG_STRIDE;
-#ifdef GSV_TOP_TRACE
-    uint64_t t_start = __builtin_amdgcn_s_memtime(), t_lv[TOP_MAX_H + 1];
-#endif
     for (int h = tl.h0; h <= tl.h1; h++) {
         int hb = tl.hb[h - 1], he = tl.he[h - 1];
         int gb = tl.gb[h - 1], ge = tl.ge[h - 1];
@@ -1043,20 +883,7 @@ __global__ __launch_bounds__(TOP_BLOCK) GSV_TOP_ATTR void k_chunk_top(const PNod
             }
         }
         __syncthreads();
-#ifdef GSV_TOP_TRACE
-        t_lv[h] = __builtin_amdgcn_s_memtime();
-#endif
     }
-#ifdef GSV_TOP_TRACE
-    if (blockIdx.x == 0 && tid == 0) {
-        uint64_t prev = t_start;
-        for (int h = tl.h0; h <= tl.h1; h++) {
-            printf("top h=%d hfull=%d gen=%d ticks=%llu\n", h, tl.he[h - 1] - tl.hb[h - 1], tl.ge[h - 1] - tl.gb[h - 1],
-                   (unsigned long long)(t_lv[h] - prev));
-            prev = t_lv[h];
-        }
-    }
-#endif
 }
 
 // ================================================================ launcher
@@ -1070,14 +897,7 @@ size_t chunk_root_scratch_bytes(const TriePlan* plan, uint32_t nbodies) {
 // bulk kernels there): right after the bottom level (r05 default), so the next batch's bottom level
 // runs beside this batch's HFULL level(s) as well as its fused top — the HFULL launch of a 100-body
 // batch is ~400 waves, under half a wave per SIMD.  configs[2] 91.4-91.6 -> 93.4-94.2 GB/s at depth 2
-// and 3 (profiles/r05/ab/chunk_tail_bottom.txt).  GSV_CHUNK_TAIL_BOTTOM = 0 marks before the top (r04).
-static bool tail_after_bottom() {
-    static const bool v = [] {
-        const char* e = getenv("GSV_CHUNK_TAIL_BOTTOM");
-        return !e || atoi(e) != 0;
-    }();
-    return v;
-}
+// and 3 (profiles/r05/ab/chunk_tail_bottom.txt; through r04 the mark was before the top).
 // all heights of the plan: per-height launches below top_h, then one fused launch
 static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipStream_t st,
                                 void (*timer_begin)(void*, int), void (*timer_end)(void*, int), void* tctx) {
@@ -1111,15 +931,13 @@ static hipError_t launch_levels(const TriePlan* plan, const BodyBatch& bb, hipSt
         if (timer_end) timer_end(tctx, kid);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        if (bot && tail_after_bottom() && timer_begin) timer_begin(tctx, GSV_HOOK_TAIL);
+        if (bot && timer_begin) timer_begin(tctx, GSV_HOOK_TAIL);
     }
     if (top_h <= p.height) {
         if (p.height > TOP_MAX_H) return hipErrorInvalidValue;
-        if (!tail_after_bottom() && timer_begin) timer_begin(tctx, GSV_HOOK_TAIL);
         TopLevels tl{};
         tl.h0 = top_h;
         tl.h1 = p.height;
-        tl.prio = top_prio();
         for (int h = 1; h <= p.height; h++) {
             tl.hb[h - 1] = p.lvl_hfull_begin[h - 1];
             tl.he[h - 1] = p.lvl_hfull_end[h - 1];

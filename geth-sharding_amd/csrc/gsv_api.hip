@@ -90,13 +90,15 @@ struct Shape {
     size_t np = 0, nl = 0, nchecks = 0;
     int layout = 0;  // GSV_BN_LAYOUT_* flags
     size_t o_src = 0, o_pidx = 0, o_lfirst = 0, o_clane = 0, o_cbad = 0, o_pstat = 0, o_lines = 0,
-           o_lstat = 0, o_fv = 0, o_luse = 0, o_fws = 0;
+           o_lstat = 0, o_fv = 0, o_fws = 0;
     uint32_t maxl = 1;  // the most Miller lanes of any check
     bool deep = false;  // laid out for three or more batches in flight (pairing_shape's depth >= 3)
-    // GSV_BN_LAYOUT_CONC: per instance, the side stream and fork/join events (created at prepare)
+    // per instance, the side stream and fork/join events of a shape that runs two launch chains at
+    // once (the notary's chunk roots; the pairing's concurrent layout), created at prepare
     std::vector<hipStream_t> side;
     std::vector<hipEvent_t> efork, ejoin;
-    bool side_borrowed = false;  // host-path shape: the context's side events too, not its own
+    bool side_borrowed = false;  // host-path shape: the context's side stream and events, not its own
+    int* side_queues = nullptr;  // prepared shape: the context's count of live side queues (own streams)
     // SK_NOTARY
     uint32_t max_txs = 0, sfx_len = 0;
     int signer_kind = 0;
@@ -119,13 +121,26 @@ struct Shape {
     Shape() = default;
     Shape(const Shape&) = delete;
     Shape& operator=(const Shape&) = delete;
-    ~Shape() {
+    // the shape's own side streams (hardware queues) and events; a borrowed set stays the context's
+    void release_side() {
         if (!side_borrowed) {
+            for (hipStream_t q : side)
+                if (q) {
+                    hipStreamSynchronize(q);
+                    hipStreamDestroy(q);
+                    if (side_queues) --*side_queues;
+                }
             for (hipEvent_t e : efork)
                 if (e) hipEventDestroy(e);
             for (hipEvent_t e : ejoin)
                 if (e) hipEventDestroy(e);
-        }  // the side streams are the context's (gsv_ctx::sides) or, host path, its hside
+        }
+        side.clear();
+        efork.clear();
+        ejoin.clear();
+    }
+    ~Shape() {
+        release_side();
         for (hipEvent_t e : ev)
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : bulk_ev)
@@ -143,6 +158,11 @@ struct Shape {
 };
 
 constexpr size_t kMaxShapes = 32;
+// side streams on hardware queues of their own, over all of a context's prepared shapes: the hardware
+// scheduler time-slices queues beyond what it maps at once (r05: ~40 leaked queues ran an 8,192-check
+// pairing pipeline at 8.6 instead of 3.8 ms, profiles/r05/ab/pairing_depth_dedicated_leaked_queues.txt);
+// a shape prepared past the bound runs its chains one after the other on the caller's stream
+constexpr int kMaxSideQueues = 8;
 constexpr size_t kMaxShapeBytes = (size_t)32 << 30;  // of the 288 GB of HBM
 
 }  // namespace
@@ -183,10 +203,13 @@ struct gsv_ctx {
     // the host paths' side stream and fork/join events (lent to their per-call shapes)
     hipStream_t hside = nullptr;
     hipEvent_t hfork = nullptr, hjoin = nullptr;
-    // the prepared shapes' side streams, per instance index, on hardware queues of their own
-    // (own_queue_stream: HIP's four shared in-order queues would order a side chain after unrelated
+    // live side streams of the prepared shapes (each shape owns its own, on hardware queues of their
+    // own, own_queue_stream: HIP's four shared in-order queues would order a side chain after unrelated
     // work; the notary pipeline two deep measured 11,734 vs 11,419 shards/s, profiles/r05/ab/notary_sweep_*)
-    std::vector<hipStream_t> sides;
+    int side_queues = 0;
+    // streams made by gsv_stream_create, destroyed by gsv_stream_destroy or with the context
+    std::vector<hipStream_t> user_streams;
+    std::mutex qmu;
     int pipeline_depth = 1;  // instances per prepared shape (gsv_ctx_set_pipeline_depth)
 };
 
@@ -574,7 +597,11 @@ void gsv_ctx_destroy(gsv_ctx* c) {
     drain_timing(c);
     for (auto e : c->free_events) hipEventDestroy(e);
     c->shapes.clear();
-    for (hipStream_t q : c->sides) hipStreamDestroy(q);
+    {
+        std::lock_guard<std::mutex> g(c->qmu);
+        for (hipStream_t q : c->user_streams) hipStreamDestroy(q);
+        c->user_streams.clear();
+    }
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->coll_ev) hipEventDestroy(c->coll_ev);
     if (c->hfork) hipEventDestroy(c->hfork);
@@ -596,21 +623,41 @@ int gsv_ctx_set_timing(gsv_ctx* c, int enable) {
 // deep at 6.0 or 3.75 ms per batch by which of torch's pool streams the caller took (two of the three on
 // one HSA queue in the kernel trace), 3.75 on every set of CU-masked streams
 // (profiles/r05/ab/stream_sets_*).
+// The context owns them: at most GSV_MAX_STREAMS live at once (more queues oversubscribe the hardware
+// scheduler), and gsv_ctx_destroy destroys the ones the caller did not, before the runtime's own teardown.
 int gsv_stream_create(gsv_ctx* c, void** stream_out) {
     if (!c || !stream_out) return GSV_E_INVALID_ARG;
     *stream_out = nullptr;
+    std::lock_guard<std::mutex> g(c->qmu);
+    if (c->user_streams.size() >= GSV_MAX_STREAMS) return GSV_E_INVALID_ARG;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t q = nullptr;
     int rc = own_queue_stream(c->device, &q);
     if (rc) return rc;
+    c->user_streams.push_back(q);
     *stream_out = (void*)q;
     return GSV_SUCCESS;
 }
 
 int gsv_stream_destroy(gsv_ctx* c, void* stream) {
     if (!c || !stream) return GSV_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->qmu);
+    auto it = std::find(c->user_streams.begin(), c->user_streams.end(), (hipStream_t)stream);
+    if (it == c->user_streams.end()) return GSV_E_INVALID_ARG;  // not this context's (or already destroyed)
+    c->user_streams.erase(it);
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamDestroy((hipStream_t)stream));
+    return GSV_SUCCESS;
+}
+
+int gsv_ctx_stream_count(gsv_ctx* c, int* user_streams, int* side_streams) {
+    if (!c) return GSV_E_INVALID_ARG;
+    {
+        std::lock_guard<std::mutex> g(c->qmu);
+        if (user_streams) *user_streams = (int)c->user_streams.size();
+    }
+    std::lock_guard<std::mutex> g(c->smu);
+    if (side_streams) *side_streams = c->side_queues;
     return GSV_SUCCESS;
 }
 
@@ -863,17 +910,6 @@ bool bn_miller2(size_t nlanes, int cus, int depth) {
     if (const char* e = getenv("GSV_BN_MILLER2")) return atoi(e) != 0;
     return depth < 3 && 2 * nlanes <= (size_t)std::max(cus, 1) * 4 * 64;
 }
-// GSV_BN_LAYOUT_CONC, below about one wave per SIMD: the lines kernel at a one-wave register budget (no
-// spills), and in the BN_SUB_FROB = 0 build the curve / subgroup checks on a side stream beside it and
-// the Miller loop.  GSV_BN_CONC = 0/1 forces the choice (A/B timing).
-// In the default (BN_SUB_FROB) build the layout only picks the lines kernel at a one-wave register budget,
-// which has no spills; at 65,536 checks it takes the same time as the two-wave k_bn_prepare (7.27 vs
-// 7.26 ms, profiles/r04) without its 696 B/lane of spill traffic, so it is used at every size.
-bool bn_conc(size_t npairs, int cus) {
-    if (const char* e = getenv("GSV_BN_CONC")) return atoi(e) != 0;
-    if (!gsv::bn256_layout_forks()) return true;
-    return npairs <= (size_t)std::max(cus, 1) * 4 * 64 * 1;
-}
 // The Miller loop at two waves per SIMD (k_bn_miller_w2: one F_p^6 value per lane in LDS, products one
 // output coordinate at a time) or at one (k_bn_miller, the default).  The two-wave kernel measured
 // slower at every batch size (r05: 65,536 checks at k = 2 11.2 vs 9.8 ms of Miller, k = 4 17.0 vs
@@ -1003,7 +1039,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.deep = depth >= 3;
     s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
                (bn_miller2(s.nl, cus, depth) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
-               (np && bn_conc(np, cus) ? gsv::GSV_BN_LAYOUT_CONC : 0) | (bn_miller_w2() ? gsv::GSV_BN_LAYOUT_MILLERW2 : 0) |
+               (bn_miller_w2() ? gsv::GSV_BN_LAYOUT_MILLERW2 : 0) |
                (bn_lines_w2(np, cus) ? gsv::GSV_BN_LAYOUT_LINESW2 : 0) | (bn_miller_l() ? gsv::GSV_BN_LAYOUT_MILLERL : 0);
     s.o_src = L.add(np * 8 + 8);
     s.o_pidx = L.add(np * 4 + 4);
@@ -1019,7 +1055,6 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     const size_t fws_bytes = n * 108 * 4 * gsv::BN_FINAL_SLOTS;
     s.o_lines = L.add(std::max(lines_bytes, fws_bytes) + 4);
     s.o_lstat = L.add(s.nl + 1);
-    s.o_luse = L.add(np + 1);
     s.o_fv = L.add(s.nl * 108 * 4 + 4);
     s.o_fws = s.o_lines;
     s.stage(s.o_src, pair_src.data(), np);
@@ -1029,37 +1064,29 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.stage(s.o_cbad, bad_len.data(), n);
     return GSV_SUCCESS;
 }
-// a side stream and fork/join events per instance (at prepare / host-path build), for shapes that run
-// two independent launch chains at once: the pairing's concurrent layout, the notary's chunk roots
+// a side stream and fork/join events per instance (at prepare), for shapes that run two independent
+// launch chains at once: the notary's chunk roots (and the pairing's concurrent layout).  The streams are
+// the SHAPE's own, on hardware queues of their own (a context-wide pool let an uncaptured call
+// of one shape enqueue onto a side stream another shape's capture had joined); they live until the shape
+// is evicted or retired.  Past kMaxSideQueues live side queues, or when HIP refuses a stream or event, the
+// shape gets no side streams and runs its chains one after the other on the caller's stream: the results
+// are the same and the prepare succeeds (gsv.h).
 int shape_side_init(gsv_ctx* c, Shape& s) {
     if (!s.side.empty()) return GSV_SUCCESS;
-    std::vector<hipStream_t> side(s.ninst, nullptr);
-    std::vector<hipEvent_t> efork(s.ninst, nullptr), ejoin(s.ninst, nullptr);
-    int rc = GSV_SUCCESS;
-    for (int k = 0; k < s.ninst && !rc; k++) {
-        // instance k's side stream: the context's k-th, on a hardware queue of its own (shared by the
-        // shapes: only their side chains on one instance index are ordered after each other)
-        while (!rc && (int)c->sides.size() <= k) {
-            hipStream_t q = nullptr;
-            rc = own_queue_stream(c->device, &q);
-            if (!rc) c->sides.push_back(q);
-        }
-        if (rc) break;
-        side[k] = c->sides[k];
-        if (hipEventCreateWithFlags(&efork[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ejoin[k], hipEventDisableTiming) != hipSuccess)
-            rc = GSV_E_HIP;
+    if (c->side_queues + s.ninst > kMaxSideQueues) return GSV_SUCCESS;  // serial chains
+    s.side.assign(s.ninst, nullptr);
+    s.efork.assign(s.ninst, nullptr);
+    s.ejoin.assign(s.ninst, nullptr);
+    s.side_queues = &c->side_queues;
+    bool ok = true;
+    for (int k = 0; k < s.ninst && ok; k++) {
+        ok = own_queue_stream(c->device, &s.side[k]) == GSV_SUCCESS;
+        if (ok) c->side_queues++;
+        else s.side[k] = nullptr;
+        ok = ok && hipEventCreateWithFlags(&s.efork[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&s.ejoin[k], hipEventDisableTiming) == hipSuccess;
     }
-    if (rc) {  // no partial set: a shape without side streams runs its chains on the caller's stream
-        for (hipEvent_t e : efork)
-            if (e) hipEventDestroy(e);
-        for (hipEvent_t e : ejoin)
-            if (e) hipEventDestroy(e);
-        return rc;
-    }
-    s.side = std::move(side);
-    s.efork = std::move(efork);
-    s.ejoin = std::move(ejoin);
+    if (!ok) s.release_side();  // no partial set
     return GSV_SUCCESS;
 }
 // a host-path (per-call) shape borrows the context's side stream and events instead of creating its own
@@ -1076,32 +1103,15 @@ int shape_side_borrow(gsv_ctx* c, Shape& s) {
     s.side_borrowed = true;
     return GSV_SUCCESS;
 }
-// the concurrent layout forks onto a side stream only in the BN_SUB_FROB = 0 build (check waves)
-int pairing_conc_init(gsv_ctx* c, Shape& s, bool host_path) {
-    if (!(s.layout & gsv::GSV_BN_LAYOUT_CONC) || !gsv::bn256_layout_forks()) return GSV_SUCCESS;
-    return host_path ? shape_side_borrow(c, s) : shape_side_init(c, s);
-}
 int pairing_run(gsv_ctx* c, const Shape& s, const uint8_t* d_in, uint8_t* d_verdict, hipStream_t st) {
-    gsv::BnConcurrent conc{};
-    const gsv::BnConcurrent* pc = nullptr;
-    if ((s.layout & gsv::GSV_BN_LAYOUT_CONC) && (size_t)s.cur < s.side.size()) {
-        conc = gsv::BnConcurrent{s.side[s.cur], s.efork[s.cur], s.ejoin[s.cur], s.at<uint8_t>(s.o_luse)};
-        pc = &conc;
-    }
-    // without a side stream the concurrent layout can only keep its kernel choice (the one-wave lines
-    // kernel), which is all it is in the default build (bn256_layout_forks() false)
-    int layout = (pc || !gsv::bn256_layout_forks()) ? s.layout : (s.layout & ~gsv::GSV_BN_LAYOUT_CONC);
     return hip_err(gsv::launch_bn256_pairing(
         d_in, s.at<uint64_t>(s.o_src), (uint32_t)s.np, s.at<uint32_t>(s.o_lfirst), s.at<uint32_t>(s.o_pidx),
         (uint32_t)s.nl, s.at<uint32_t>(s.o_clane), s.at<uint8_t>(s.o_cbad), (uint32_t)s.nchecks,
         s.at<uint8_t>(s.o_pstat), s.at<uint32_t>(s.o_lines), s.at<uint8_t>(s.o_lstat),
-        s.at<uint32_t>(s.o_fv), s.at<uint32_t>(s.o_fws), s.maxl, d_verdict, layout, st, hook_begin, hook_end, c, pc));
+        s.at<uint32_t>(s.o_fv), s.at<uint32_t>(s.o_fws), s.maxl, d_verdict, s.layout, st, hook_begin, hook_end, c));
 }
 
 // ---- notary: key = chain id, signer, max_txs, body offsets
-#ifndef GSV_NOTARY_FORK
-#define GSV_NOTARY_FORK 1
-#endif
 std::vector<uint64_t> notary_key(const uint64_t* h_off, size_t n, const uint8_t* cid, size_t cidlen, int signer,
                                  uint32_t max_txs) {
     std::vector<uint64_t> k{(uint64_t)signer, max_txs};
@@ -1158,7 +1168,12 @@ int notary_run(gsv_ctx* c, const Shape& s, size_t n, const uint8_t* d_bodies, ui
     // The chunk roots of the same bodies are independent of the transactions: with a side stream they
     // run beside the blob decode + recovery (fork / join by events, so a capture still works) and
     // fill the SIMDs the recovery kernel's tail and the trie top leave idle.
-    const bool fork = GSV_NOTARY_FORK && (size_t)s.cur < s.side.size();
+    // The chunk roots fork onto the shape's side stream when it has one (r03: +3.3 % against the serial
+    // form, profiles/r03/ab_notary_fork.txt; r05: 11,491 vs 11,233 shards/s, profiles/r05/ab/notary_fork*.json)
+    const bool fork = (size_t)s.cur < s.side.size();
+    // The pipelined step's mark for the next step (GSV_HOOK_TAIL, shape_run) is the chunk root's, after
+    // its bottom level.  r06 A/B at 13 / 25 / 100 shards, depth 2-4: no mark, or a mark after the blob
+    // index, measured the same (profiles/r06/ab/notary_stagger_steps.txt).
     if (fork) {
         HIPCHK(hipEventRecord(s.efork[s.cur], st));
         HIPCHK(hipStreamWaitEvent(s.side[s.cur], s.efork[s.cur], 0));
@@ -1385,8 +1400,10 @@ int shape_get(gsv_ctx* c, uint64_t kind, std::vector<uint64_t>&& key, B&& build,
     if (s && (s->ninst < c->pipeline_depth || reclass)) {
         // prepared before the depth was raised (or at the other depth class): build a new one, and
         // RETIRE the old one instead of freeing it (it is never found again but keeps its memory until
-        // LRU eviction, which drains its queued work first), so a graph captured from it stays valid
+        // LRU eviction, which drains its queued work first), so a graph captured from it stays valid.
+        // Its side streams go now (a captured graph holds no streams): the new shape needs the queues.
         s->kind |= 1ull << 63;
+        s->release_side();
         s = nullptr;
     }
     if (!s) {
@@ -1594,8 +1611,7 @@ int gsv_bn256_pairing_prepare(gsv_ctx* c, const uint64_t* h_off, size_t n) {
     const int depth = std::max(1, c->pipeline_depth);
     int rc = shape_get(c, SK_PAIRING, pairing_key(h_off, n),
                        [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, h_off, n, L, depth); }, &s);
-    if (rc) return rc;
-    return pairing_conc_init(c, *s, false);
+    return rc;
 }
 
 int gsv_bn256_pairing_check_batch_dev(gsv_ctx* c, const uint8_t* d_in, const uint64_t* h_off, size_t n,
@@ -1628,8 +1644,6 @@ int gsv_bn256_pairing_check_batch(gsv_ctx* c, const uint8_t* in, const uint64_t*
     size_t staged = al(bytes + 8) + al(n);
     Shape s;
     int rc = shape_temp(c, staged, [&](Shape& ns, Layout& L) { return pairing_shape(c, ns, rel.data(), n, L, 1); }, s);
-    if (rc) return rc;
-    rc = pairing_conc_init(c, s, true);
     if (rc) return rc;
     Carve cv(c->arena);
     uint8_t* d_in = cv.take<uint8_t>(bytes + 8);

@@ -54,17 +54,11 @@ hipError_t launch_header_verify(const uint8_t* d_sid32, const uint8_t* d_root32,
                                 uint8_t* d_status, hipStream_t st);
 
 // layout flags of launch_bn256_pairing: the final exponentiation on three lanes per check and the Miller
-// loop on two lanes per Miller lane (batches below one wave per SIMD), the one-wave lines kernel
-// (CONC), the two-wave lines kernel (LINESW2, large batches), and the two-wave Miller kernels kept for
-// A/B (MILLERW2, MILLERL; off by default)
-constexpr int GSV_BN_LAYOUT_FINAL3 = 1, GSV_BN_LAYOUT_MILLER2 = 2, GSV_BN_LAYOUT_CONC = 4, GSV_BN_LAYOUT_MILLERW2 = 8,
+// loop on two lanes per Miller lane (batches below one wave per SIMD), the two-wave lines kernel
+// (LINESW2, large batches; else the one-wave k_bn_lines), and the two-wave Miller kernels kept for A/B
+// (MILLERW2, MILLERL; off by default)
+constexpr int GSV_BN_LAYOUT_FINAL3 = 1, GSV_BN_LAYOUT_MILLER2 = 2, GSV_BN_LAYOUT_MILLERW2 = 8,
               GSV_BN_LAYOUT_LINESW2 = 16, GSV_BN_LAYOUT_MILLERL = 32;
-// the concurrent layout's side stream, fork/join events and the lines role's per-pair use flags
-struct BnConcurrent {
-    hipStream_t side;
-    hipEvent_t fork, join;
-    uint8_t* d_luse;
-};
 // bn256.hip: pairs in slot-major order (the j-th pairs of all checks contiguous): pair_src[p] = byte
 // offset of pair p in d_in.  A check's pairs are split into Miller lanes of <= k pairs each: lane l
 // runs the multi-Miller loop over pidx[lane_first[l] .. lane_first[l+1]), check c owns lanes
@@ -79,11 +73,7 @@ hipError_t launch_bn256_pairing(const uint8_t* d_in, const uint64_t* d_pair_src,
                                 const uint32_t* d_check_lane, const uint8_t* d_cbad, uint32_t nchecks,
                                 uint8_t* d_pstat, uint32_t* d_lines, uint8_t* d_lstat, uint32_t* d_fv,
                                 uint32_t* d_fws, uint32_t maxl, uint8_t* d_verdict, int layout, hipStream_t st, void (*timer_begin)(void*, int),
-                                void (*timer_end)(void*, int), void* tctx, const BnConcurrent* conc);
-
-// false in the default build: the concurrent layout only picks the one-wave lines kernel and nothing
-// forks onto a side stream (true in the BN_SUB_FROB = 0 build, whose check waves run beside the lines)
-bool bn256_layout_forks();
+                                void (*timer_end)(void*, int), void* tctx);
 hipError_t launch_bn256_synth(uint64_t seed, uint32_t nchecks, uint8_t* d_out, uint8_t* d_expect, hipStream_t st);
 
 // notary.hip
@@ -110,10 +100,7 @@ hipError_t launch_notary_synth(uint64_t seed, uint32_t shard0, uint32_t n_shards
 // window, prefetched a window ahead); 16-bit: 16 adds, 80 MiB (Infinity-Cache resident), 1.3 % slower;
 // 22-bit: 12 adds, 4 GB, within 0.1 % of 20-bit (profiles/r02/ab_comb.txt).  The table is built once
 // per context (k_gtable_base + k_gtable_init).
-#ifndef GSV_COMB_BITS
-#define GSV_COMB_BITS 20
-#endif
-constexpr int COMB_BITS = GSV_COMB_BITS;
+constexpr int COMB_BITS = 20;
 constexpr int COMB_WINDOWS = (256 + COMB_BITS - 1) / COMB_BITS;  // the top window may be partial
 static_assert(COMB_BITS >= 4 && COMB_BITS <= 26, "comb window width");
 constexpr size_t GTAB_ENTRIES = (size_t)COMB_WINDOWS << COMB_BITS;

@@ -21,13 +21,11 @@ __device__ constexpr uint64_t KECCAK_RC[24] = {
     0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
 
 // v_bitop3_b32 truth tables (index = S0<<2 | S1<<1 | S2): S0^S1^S2, and chi's S0 ^ (~S1 & S2)
-#ifndef GSV_BITOP3_CHI
-#define GSV_BITOP3_CHI 0xD2
-#endif
 constexpr uint32_t BITOP3_XOR3 = 0x96;
+constexpr uint32_t BITOP3_CHI = 0xD2;
 
 GSV_DI uint32_t kxor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, BITOP3_XOR3); }
-GSV_DI uint32_t kchi(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, GSV_BITOP3_CHI); }
+GSV_DI uint32_t kchi(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, BITOP3_CHI); }
 
 // 64-bit rotate-left by R of (hi:lo): two v_alignbit_b32 (rotates by 0/32 are register renames)
 template <int R>
@@ -52,36 +50,24 @@ __device__ constexpr int KECCAK_RHO[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 2
                                            25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
 
 // theta's D[x] = C[x - 1] ^ rot(C[x + 1], 1) is applied as ONE three-input XOR per word,
-// A ^ C[x - 1] ^ rot(C[x + 1], 1) (GSV_KECCAK_THETA3 = 1, r05): 50 v_bitop3 instead of 10 v_xor for D
-// plus 50 v_xor, i.e. the round at the 180-instruction floor.  0: D first (through r04).
-#ifndef GSV_KECCAK_THETA3
-#define GSV_KECCAK_THETA3 1
-#endif
+// A ^ C[x - 1] ^ rot(C[x + 1], 1) (r05): 50 v_bitop3 instead of 10 v_xor for D plus 50 v_xor (through
+// r04), i.e. the round at the 180-instruction floor (profiles/r05/ab/keccak_theta3.txt).
 template <int I>
 GSV_DI void theta_rho_pi(uint32_t bl[25], uint32_t bh[25], const uint32_t al[25], const uint32_t ah[25],
                          const uint32_t dl[5], const uint32_t dh[5], const uint32_t cl[5], const uint32_t ch[5]) {
     constexpr int x = I % 5, y = I / 5;
     constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
-#if GSV_KECCAK_THETA3
-    // dl / dh hold rot(C[x + 1], 1) here
+    // dl / dh hold rot(C[x + 1], 1)
     krot<KECCAK_RHO[I]>(bl[dst], bh[dst], kxor3(al[I], cl[(x + 4) % 5], dl[x]), kxor3(ah[I], ch[(x + 4) % 5], dh[x]));
-#else
-    krot<KECCAK_RHO[I]>(bl[dst], bh[dst], al[I] ^ dl[x], ah[I] ^ dh[x]);
-#endif
     if constexpr (I + 1 < 25) theta_rho_pi<I + 1>(bl, bh, al, ah, dl, dh, cl, ch);
 }
 
-// rounds per loop iteration (GSV_KECCAK_UNROLL, A/B; 1 = one round per iteration; 2 measured equal, r05)
-#ifndef GSV_KECCAK_UNROLL
-#define GSV_KECCAK_UNROLL 1
-#endif
-#define GSV_PRAGMA(x) _Pragma(#x)
-#define GSV_UNROLL(n) GSV_PRAGMA(unroll n)
 // One full permutation over the state split into 32-bit halves (lane index x + 5y).  Per round:
 // theta's column parities as 20 three-way v_bitop3, rot(C, 1) as 10 v_alignbit, theta's application as
-// 50 three-way v_bitop3, rho as 48 v_alignbit, chi as 50 v_bitop3, iota 2.
+// 50 three-way v_bitop3, rho as 48 v_alignbit, chi as 50 v_bitop3, iota 2.  One round per loop
+// iteration (two measured equal, r05: profiles/r05/ab/chunk_levels5_unroll2.txt).
 GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) {
-    GSV_UNROLL(GSV_KECCAK_UNROLL)
+#pragma unroll 1
     for (int round = 0; round < 24; round++) {
         uint32_t cl[5], ch[5], dl[5], dh[5];
 #pragma unroll
@@ -93,13 +79,8 @@ GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) {
         for (int x = 0; x < 5; x++) {
             uint32_t rl, rh;
             krot<1>(rl, rh, cl[(x + 1) % 5], ch[(x + 1) % 5]);
-#if GSV_KECCAK_THETA3
             dl[x] = rl;
             dh[x] = rh;
-#else
-            dl[x] = cl[(x + 4) % 5] ^ rl;
-            dh[x] = ch[(x + 4) % 5] ^ rh;
-#endif
         }
         uint32_t bl[25], bh[25];
         theta_rho_pi<0>(bl, bh, al, ah, dl, dh, cl, ch);

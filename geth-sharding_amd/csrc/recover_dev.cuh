@@ -33,59 +33,35 @@ __device__ constexpr uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75F
 __device__ constexpr uint32_t HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
                                            0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
 
-// u2 R's GLV halves are recoded into fixed-schedule odd digits of GSV_GLV_W bits: digits in
+// u2 R's GLV halves are recoded into fixed-schedule odd digits of GLV_W bits: digits in
 // {+-1, +-3, ..., +-(2^W - 1)}, a table of the 2^(W-1) odd multiples of R, W doublings per digit.
-#ifndef GSV_GLV_W
-#define GSV_GLV_W 4
-#endif
-constexpr int GLV_W = GSV_GLV_W;
+// (w = 5 measured slower, r02-r05: DESIGN.md §7.3)
+constexpr int GLV_W = 4;
 constexpr int GLV_NT = 1 << (GLV_W - 1);             // table entries
-constexpr int GLV_DIGITS = (130 + GLV_W - 1) / GLV_W;  // |k| < 2^130: the split gives < 2^128, + skew or a lattice vector (GSV_GLV_ODD) < 2^129.3
+constexpr int GLV_DIGITS = (130 + GLV_W - 1) / GLV_W;  // |k| < 2^130: the split gives < 2^128, + a lattice vector (glv_make_odd) < 2^129.3
 // digit code = sign bit above a (W - 1)-bit table index, packed in DIG_SLOT-bit slots
 constexpr int DIG_SLOT = GLV_W <= 4 ? 4 : 8;
 constexpr int DIG_PER_WORD = 32 / DIG_SLOT;
 constexpr int DIG_WORDS = (GLV_DIGITS + DIG_PER_WORD - 1) / DIG_PER_WORD;
 static_assert(GLV_W >= 3 && GLV_W <= 5, "GLV window width");
-// where the per-lane GLV table lives: 0 = LDS ([word][256 lanes] per block), 1 = a private array
-// (scratch: memory only for resident lanes, served by L1/L2), 2 = entries 0..3 in LDS and the rest
-// in the private array.  Two waves per SIMD leave LDS room for 72 words a lane: four entries.
-#ifndef GSV_GLV_TAB
-#define GSV_GLV_TAB (GLV_W == 3 ? 0 : 2)
-#endif
-constexpr int GLV_LNT = GSV_GLV_TAB == 1 ? 0 : GSV_GLV_TAB == 2 ? 4 : GLV_NT;  // entries in LDS
-static_assert(GLV_LNT <= 4 && GLV_LNT <= GLV_NT, "LDS holds at most four entries at two waves per SIMD");
+// where the per-lane GLV table lives: entries 0..3 in LDS ([word][256 lanes] per block), the rest in a
+// private array (scratch: memory only for resident lanes, served by L1/L2).  Two waves per SIMD leave
+// LDS room for 72 words a lane: four entries.  (The whole table private measured 107.2 vs 113.7-114.3 M
+// recoveries/s, r05: profiles/r05/ab/ecrecover_options.txt.)
+constexpr int GLV_LNT = 4;  // entries in LDS
+static_assert(GLV_LNT <= GLV_NT, "LDS holds at most four entries at two waves per SIMD");
 // LDS part: 18 GLV_LNT words per lane, lane-minor ([word][GSV_LTAB_STRIDE]); the kernels that call
 // recover_core run 256-thread blocks and declare __shared__ uint32_t[GSV_LTAB_WORDS].
 constexpr int GSV_LTAB_STRIDE = 256;
 constexpr int GSV_LTAB_WORDS = 18 * GLV_LNT * GSV_LTAB_STRIDE;
-// 1: the lambda half's x coordinates (beta x_e) precomputed per entry in a private array instead of
-// one product per lambda add: +0.3 % (profiles/r02/ab_betatab.txt), but the per-lane entry index
-// scatters the private-array reads over cache lines: 4.6x the kernel's fetch bytes (1.65 -> 7.6 GB
-// per 2^20 recoveries).  Off.
-#ifndef GSV_GLV_BETA_TAB
-#define GSV_GLV_BETA_TAB 0
-#endif
-// 1: the private-array half of the GLV table is read one add AHEAD (software prefetch): its scratch
-// loads (L2/MALL latency) run under the current add instead of stalling it; every lane reads both
-// halves at index (e & 3) and selects (no divergent branch).  GSV_GLV_TAB == 2 only.
-#ifndef GSV_GLV_PREFETCH
-#define GSV_GLV_PREFETCH 0
-#endif
-// 1: the two adds of a digit position (k1 on T, k2 on lambda T) as straight-line code (A/B)
-#ifndef GSV_GLV_UNROLL_J
-#define GSV_GLV_UNROLL_J 0
-#endif
+// Measured and not kept (r02-r05): the lambda half's x coordinates (beta x_e) precomputed per entry in
+// a private array (+0.3 %, but 4.6x the fetch bytes: profiles/r02/ab_betatab.txt), the private half
+// read one add ahead (112.3-112.8 vs 113.7-114.3 M/s) and the two adds of a digit position as
+// straight-line code (equal) (profiles/r05/ab/ecrecover_options.txt).
 // waves per SIMD the recovery kernels are compiled for (register budget 512 / waves)
-#ifndef GSV_ECR_WAVES
 #define GSV_ECR_WAVES 2
-#endif
-#if GSV_GLV_TAB != 1
 #define GSV_LTAB_DECL __shared__ uint32_t ltab[GSV_LTAB_WORDS]
 #define GSV_LTAB_LANE (ltab + threadIdx.x)
-#else
-#define GSV_LTAB_DECL
-#define GSV_LTAB_LANE nullptr
-#endif
 
 // ---------------------------------------------------------------------------- scalar helpers
 GSV_DI void sc_from_const(sc& r, const uint32_t c[8]) {
@@ -314,16 +290,13 @@ GSV_DI void gej9_to_affine_words(fe& ax, fe& ay, const gej9& q) {
     fe9_to_words(ay.v, y);
 }
 
-// 1 (default): u2 R runs on the curve E_t: y^2 = x^3 + 7 c^3 (c = x_R^3 + 7), the image of E under
+// u2 R runs on the curve E_t: y^2 = x^3 + 7 c^3 (c = x_R^3 + 7), the image of E under
 // (x, y) -> (t^2 x, t^3 y) for t = y_R, where R is (c x_R, c^2) whatever t is, so no square root is
 // taken before the scalar multiplication.  A Jacobian (X, Y, Z) on E_t is (X, Y, t Z) on E; the sum with
 // u1 G is carried as a + t b, and ONE exponentiation at the end, w = (c z^4)^((p-3)/4) = 1/(s0 z^2)
 // with s0 = c^((p+1)/4), yields the root (s0 = c w z^2, t = +-s0 by the recid parity) and the inverse of
-// Z (1/(s0 z) = w z): the separate Z^-1 safegcd is gone.  0: the square root first, then the affine
-// conversion by safegcd (the round-3 form).
-#ifndef GSV_RECOVER_TWIST
-#define GSV_RECOVER_TWIST 1
-#endif
+// Z (1/(s0 z) = w z): the separate Z^-1 safegcd is gone (r04; through r03 the square root came first,
+// then the affine conversion by safegcd).
 
 // Q = P1 + P2 with P1 = u1 G on E (Jacobian, inf flag p1inf) and P2 = u2 R given on E_t as (X*, Y*, Z*)
 // (P2 on E = (X*, Y*, t Z*)), c = x_R^3 + 7, par = the parity y_R must have.  Returns false when c is
@@ -444,15 +417,12 @@ GSV_DI bool recover_tail_twisted(fe& qx, fe& qy, const gej9& p1, bool p1inf, con
     return ok;
 }
 
-// 1 (default): both GLV halves are made odd before the recoding by adding a vector of the GLV lattice
+// Both GLV halves are made odd before the recoding by adding a vector of the GLV lattice
 // ({(a, b) : a + b lambda == 0 mod n}, libsecp256k1 scalar_impl.h's basis), so the odd-digit recoding
 // needs no skew and the two skew-correcting mixed adds at the end of u2 R disappear.  v1 = (a1, b1)
 // has odd/odd coordinates, v2 = (a2, a1) even/odd, v1 + v2 odd/even: one of them (or none) turns the
 // magnitudes |k1|, |k2| (parity of k mod n XOR its sign, n being odd) both odd.  |a1| < 2^126,
 // |b1| < 2^128, |a2| < 2^129: |k| < 2^128 grows below 2^129.3 < 2^130, inside GLV_DIGITS' range.
-#ifndef GSV_GLV_ODD
-#define GSV_GLV_ODD 1
-#endif
 __device__ constexpr uint32_t GLV_V1A[8] = {0x9284EB15u, 0xE86C90E4u, 0xA7D46BCDu, 0x3086D221u, 0u, 0u, 0u, 0u};
 __device__ constexpr uint32_t GLV_V1B[8] = {0xC5765C7Eu, 0x507DDEE3u, 0xAE3A1813u, 0xD66B5E10u,
                                             0xFFFFFFFDu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -506,7 +476,6 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         fe9_from_words(x, xw);
     }
     fe9 y, t;
-#if GSV_RECOVER_TWIST
     // R on E_t (see recover_tail_twisted): (c x, c^2), c = x^3 + 7; the root is taken at the end
     fe9 c;
     fe9_sqr(t, x);
@@ -515,20 +484,6 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     fe9_mul(t, c, x);
     fe9_sqr(y, c);
     x = t;
-#else
-    // y = sqrt(x^3 + 7), parity recid & 1
-    fe9_sqr(t, x);
-    fe9_mul(t, t, x);
-    t.v[0] += 7u;
-    ok = ok && fe9_sqrt(y, t);
-    {
-        fe9_normalize_full(y);
-        fe9 ny;
-        fe9_neg<1>(ny, y);
-        fe9_normalize_weak(ny);
-        fe9_cmov(y, ny, (y.v[0] & 1u) != (recid & 1u));
-    }
-#endif
     // u1 = -m / r, u2 = s / r
     sc rn, u1, u2;
     modinv30_words(rn.v, rs.v, MI30_N);  // r^-1 mod n (safegcd; r != 0 on every valid path)
@@ -539,9 +494,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     // ---- u2 * R via GLV + fixed w = GLV_W odd digits
     sc k1, k2;
     sc_split_lambda(k1, k2, u2);
-#if GSV_GLV_ODD
-    glv_make_odd(k1, k2);
-#endif
+    glv_make_odd(k1, k2);  // both halves odd: the recoding's skews are 0, no correcting adds
     bool neg1 = sc_is_high(k1), neg2 = sc_is_high(k2);
     {
         sc nk;
@@ -552,7 +505,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
 #pragma unroll
         for (int i = 0; i < 8; i++) k2.v[i] = neg2 ? nk.v[i] : k2.v[i];
     }
-    uint32_t dig1[DIG_WORDS], dig2[DIG_WORDS], skew1, skew2;
+    uint32_t dig1[DIG_WORDS], dig2[DIG_WORDS], skew1, skew2;  // skews 0 (odd halves)
     recode_glv(dig1, skew1, k1);
     recode_glv(dig2, skew2, k2);
 
@@ -617,22 +570,6 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         }
         fe9_mul(zfac, f, zd);  // f = all the z-ratios: the entries' common Z on E is zd f
     }
-#if GSV_GLV_BETA_TAB
-    uint32_t ptabB[9 * GLV_NT];  // beta x_e
-    {
-        fe9 beta;
-        fe9_from_const(beta, BETA);
-#pragma unroll
-        for (int e = 0; e < GLV_NT; e++) {
-            fe9 ex, bx;
-#pragma unroll
-            for (int k = 0; k < 9; k++) ex.v[k] = GLV_X(e, k);
-            fe9_mul(bx, ex, beta);
-#pragma unroll
-            for (int k = 0; k < 9; k++) ptabB[e * 9 + k] = bx.v[k];
-        }
-    }
-#endif
 
     gej9 acc;
     bool ainf = true;
@@ -642,62 +579,6 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         acc.y.v[k] = GLV_Y(0, k);
     }
     fe9_set_u32(acc.z, 1);
-#if GSV_GLV_PREFETCH && GSV_GLV_TAB == 2 && !GSV_GLV_BETA_TAB
-    static_assert(GLV_LNT == 4 && PNT == 4, "prefetch layout: entries 0-3 in LDS, 4-7 private");
-    {
-        constexpr uint32_t CMASK = (1u << DIG_SLOT) - 1u;
-        auto code_at = [&](int i, int j) -> uint32_t {
-            return (sel_word(j ? dig2 : dig1, (uint32_t)i / DIG_PER_WORD) >> ((i % DIG_PER_WORD) * DIG_SLOT)) & CMASK;
-        };
-        uint32_t pre[18];
-        auto prefetch = [&](uint32_t c) {
-            uint32_t xo = (c & 3u) * 9u;
-#pragma unroll
-            for (int k = 0; k < 9; k++) {
-                pre[k] = ptab[xo + k];
-                pre[9 + k] = ptab[9 * PNT + xo + k];
-            }
-        };
-        uint32_t cn = code_at(GLV_DIGITS - 1, 0);
-        prefetch(cn);
-#pragma unroll 1
-        for (int i = GLV_DIGITS - 1; i >= 0; i--) {
-            if (i != GLV_DIGITS - 1) {
-#pragma unroll 1
-                for (int d = 0; d < GLV_W; d++) gej9_dbl(acc, acc);
-            }
-#pragma unroll 1
-            for (int j = 0; j < 2; j++) {
-                uint32_t c = cn;
-                bool ng = j ? neg2 : neg1;
-                uint32_t ei = c & (uint32_t)(GLV_NT - 1);
-                bool hi = ei >= 4u;
-                uint32_t xo = (ei & 3u) * 9u;
-                ge9 P;
-#pragma unroll
-                for (int k = 0; k < 9; k++) {
-                    uint32_t lx = GLV_L(xo + k), ly = GLV_L(9u * GLV_LNT + xo + k);
-                    P.x.v[k] = hi ? pre[k] : lx;
-                    P.y.v[k] = hi ? pre[9 + k] : ly;
-                }
-                int ni = j ? i - 1 : i;  // the next add: (i, 1) or (i - 1, 0)
-                if (ni >= 0) {           // wave-uniform
-                    cn = code_at(ni, j ? 0 : 1);
-                    prefetch(cn);
-                }
-                if (j != 0) {  // wave-uniform
-                    fe9 beta;
-                    fe9_from_const(beta, BETA);
-                    fe9_mul(P.x, P.x, beta);
-                }
-                fe9 ny;
-                fe9_neg<1>(ny, P.y);
-                fe9_cmov(P.y, ny, ((c >> (GLV_W - 1)) != 0) != ng);
-                gej9_add_ge(acc, ainf, acc, P);
-            }
-        }
-    }
-#else
 #pragma unroll 1
     for (int i = GLV_DIGITS - 1; i >= 0; i--) {
         if (i != GLV_DIGITS - 1) {
@@ -708,11 +589,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
         uint32_t c1 = (sel_word(dig1, (uint32_t)i / DIG_PER_WORD) >> ((i % DIG_PER_WORD) * DIG_SLOT)) & CMASK;
         uint32_t c2 = (sel_word(dig2, (uint32_t)i / DIG_PER_WORD) >> ((i % DIG_PER_WORD) * DIG_SLOT)) & CMASK;
         // one add body, two passes: digit of k1 on T, digit of k2 on lambda(T) = (beta x, y)
-#if GSV_GLV_UNROLL_J
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
         for (int j = 0; j < 2; j++) {
             uint32_t c = j ? c2 : c1;
             bool ng = j ? neg2 : neg1;
@@ -734,14 +611,9 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
                 }
             }
             if (j != 0) {  // wave-uniform
-#if GSV_GLV_BETA_TAB
-#pragma unroll
-                for (int k = 0; k < 9; k++) P.x.v[k] = ptabB[ei * 9u + k];
-#else
                 fe9 beta;
                 fe9_from_const(beta, BETA);
                 fe9_mul(P.x, P.x, beta);
-#endif
             }
             fe9 ny;
             fe9_neg<1>(ny, P.y);         // 2
@@ -757,41 +629,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
             gej9_add_ge(acc, ainf, acc, P);
         }
     }
-#endif
-    // skew corrections: the recoded scalars were k + skew -> subtract (+-)T0 / (+-)lambda(T0)
-    // (GSV_GLV_ODD: both halves are odd, the skews are 0 and there is nothing to correct)
-#pragma unroll 1
-    for (int j = 0; j < (GSV_GLV_ODD ? 0 : 2); j++) {
-        bool ng = j ? neg2 : neg1;
-        uint32_t sk = j ? skew2 : skew1;
-        ge9 P;
-#pragma unroll
-        for (int k = 0; k < 9; k++) {
-            P.x.v[k] = GLV_X(0, k);
-            P.y.v[k] = GLV_Y(0, k);
-        }
-        if (j != 0) {
-#if GSV_GLV_BETA_TAB
-#pragma unroll
-            for (int k = 0; k < 9; k++) P.x.v[k] = ptabB[k];
-#else
-            fe9 beta;
-            fe9_from_const(beta, BETA);
-            fe9_mul(P.x, P.x, beta);
-#endif
-        }
-        fe9 ny;
-        fe9_neg<1>(ny, P.y);
-        fe9_cmov(P.y, ny, !ng);
-        gej9 tmp;
-        bool tinf = ainf;
-        gej9_add_ge(tmp, tinf, acc, P);
-        if (sk) {
-            acc = tmp;
-            ainf = tinf;
-        }
-    }
-    fe9_mul(acc.z, acc.z, zfac);  // back from E'' to E (E_t with GSV_RECOVER_TWIST; 2*1 -> 1)
+    fe9_mul(acc.z, acc.z, zfac);  // back from E'' to E_t (2*1 -> 1)
 
     // ---- u1 * G via comb
     gej9 accg;
@@ -799,15 +637,7 @@ GSV_DI uint32_t recover_core(fe& qx, fe& qy, const uint32_t msg[8], const uint32
     comb_mul_g9(accg, ginf, u1, gtab);
 
     // ---- Q = u2 R + u1 G
-#if GSV_RECOVER_TWIST
     ok = recover_tail_twisted(qx, qy, accg, ginf, acc, ainf, c, recid & 1u) && ok;
-#else
-    gej9 q;
-    bool qinf;
-    gej9_add(q, qinf, acc, ainf, accg, ginf);
-    ok = ok && !qinf;
-    gej9_to_affine_words(qx, qy, q);
-#endif
     return ok ? GSV_ST_OK : GSV_ST_RECOVER_FAILED;
 }
 

@@ -103,29 +103,17 @@ GSV_DI void fe_reduce(fe& r, const uint32_t t[16]) {
     fe_cond_sub_p(r.v, s, 0);
 }
 
-// GSV_FE_FX=1: whole-product asm statements (mul_8x8_fx / sqr_8_fx, dedicated squaring);
-// 0: the per-column statements (A/B timing only)
-#ifndef GSV_FE_FX
-#define GSV_FE_FX 1
-#endif
+// whole-product asm statements (mul_8x8_fx / sqr_8_fx, dedicated squaring)
 GSV_DI void fe_mul(fe& r, const fe& a, const fe& b) {
     GSV_OPC(OPC_FE_MUL);
     uint32_t t[16];
-#if GSV_FE_FX
     mul_8x8_fx(t, a.v, b.v);
-#else
-    mul_8x8_asm(t, a.v, b.v);
-#endif
     fe_reduce(r, t);
 }
 GSV_DI void fe_sqr(fe& r, const fe& a) {
     GSV_OPC(OPC_FE_SQR);
     uint32_t t[16];
-#if GSV_FE_FX
     sqr_8_fx(t, a.v);
-#else
-    mul_8x8_asm(t, a.v, a.v);
-#endif
     fe_reduce(r, t);
 }
 GSV_DI void fe_sqr_n(fe& r, const fe& a, int n) {

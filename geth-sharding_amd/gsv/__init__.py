@@ -11,9 +11,11 @@ fallback (a missing libgsv.so or GPU raises).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -56,15 +58,25 @@ class Context:
         self._h = h
         self.device = int(device)
         self._streams = []  # gsv_stream_create handles not yet destroyed
+        _live.add(self)
 
     # -------------------------------------------------------------- lifecycle / timing
     def close(self):
+        """Destroys the context and the streams it made (gsv_ctx_destroy also destroys any the caller left
+        live).  Every live Context is closed at interpreter exit (atexit), before the HIP runtime's own
+        static teardown, never from __del__ during module teardown."""
         if getattr(self, "_h", None):
             for q in self._streams:
                 _lib.load().gsv_stream_destroy(self._h, q)
             self._streams = []
             _lib.load().gsv_ctx_destroy(self._h)
             self._h = None
+
+    def stream_count(self):
+        """(live gsv_stream_create streams, live side streams of prepared shapes)"""
+        u, s = ctypes.c_int(), ctypes.c_int()
+        check(_lib.load().gsv_ctx_stream_count(self._h, ctypes.byref(u), ctypes.byref(s)))
+        return u.value, s.value
 
     def __del__(self):
         try:
@@ -93,8 +105,11 @@ class Context:
     def pipeline_streams(self, n: int):
         """`n` streams on hardware queues of their own (gsv_stream_create), as torch ExternalStreams: the
         streams of a pipeline of `n` batches (torch's pool streams can share an in-order queue, and
-        batches on them then serialise)."""
+        batches on them then serialise).  At most _lib.MAX_STREAMS live per context."""
         import torch
+        if len(self._streams) + int(n) > _lib.MAX_STREAMS:
+            raise GsvError(f"{len(self._streams)} pipeline streams live, {n} more exceeds GSV_MAX_STREAMS "
+                           f"({_lib.MAX_STREAMS}): destroy_streams() the previous pipeline's first")
         out = []
         for _ in range(int(n)):
             q = ctypes.c_void_p()
@@ -213,6 +228,22 @@ def _be(x: int) -> bytes:
 
 _default = None
 _default_lock = threading.Lock()
+_live = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    """Interpreter exit: close every live context (its streams, shapes, communicator) while the HIP
+    runtime is intact.  r05 record: a process that left CU-masked streams and the default context to
+    static destructors died with SIGSEGV in __cxa_finalize after rocprofv3's finalisation
+    (VERDICT r05 weak 1)."""
+    global _default
+    for c in list(_live):
+        try:
+            c.close()
+        except Exception:
+            pass
+    _default = None
 
 
 def default_context() -> Context:

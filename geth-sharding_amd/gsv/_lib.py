@@ -55,6 +55,8 @@ E_TOO_LARGE = -5
 E_RCCL = -6
 E_NOT_PREPARED = -7
 
+MAX_STREAMS = 8  # GSV_MAX_STREAMS: live gsv_stream_create streams per context
+
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -102,6 +104,7 @@ SIGNATURES = [
     ("gsv_ctx_set_pipeline_depth", ctypes.c_int, [_vp, ctypes.c_int]),
     ("gsv_stream_create", ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     ("gsv_stream_destroy", ctypes.c_int, [_vp, _vp]),
+    ("gsv_ctx_stream_count", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     ("gsv_ecrecover_precompile_batch", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("gsv_ecrecover_precompile_batch_dev", ctypes.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
     ("gsv_chunk_root_prepare", ctypes.c_int, [_vp, _vp, _sz]),

@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define GSV_ABI_VERSION 1
+#define GSV_ABI_VERSION 2 /* 2: streams owned by the context (gsv_stream_create) */
 
 /* ---- API / HIP errors (return values) ---- */
 #define GSV_SUCCESS 0
@@ -145,10 +145,21 @@ int gsv_ctx_set_pipeline_depth(gsv_ctx *ctx, int depth);
  * batches issued on them then run one after the other (including every event wait placed on them): a
  * pipeline of D batches needs D streams on D queues.  The stream is created with a CU mask of every CU
  * of the context's device (hipExtStreamCreateWithCUMask: HIP backs such a stream by a dedicated queue);
- * it is ordered with the legacy NULL stream like a hipStreamDefault stream.  Destroy it with
- * gsv_stream_destroy (after its work) before the context. */
+ * it is ordered with the legacy NULL stream like a hipStreamDefault stream (a BLOCKING stream).
+ * The context owns the stream: at most GSV_MAX_STREAMS are live per context (the next create returns
+ * GSV_E_INVALID_ARG: more queues oversubscribe the hardware scheduler), gsv_stream_destroy (after the
+ * stream's work) releases one and refuses a stream this context did not create, and gsv_ctx_destroy
+ * destroys those still live, so a process that exits without destroying its streams tears nothing down
+ * in the runtime's static-destructor order. */
+#define GSV_MAX_STREAMS 8
 int gsv_stream_create(gsv_ctx *ctx, void **stream_out);
 int gsv_stream_destroy(gsv_ctx *ctx, void *stream);
+/* Live dedicated-queue streams of the context: the caller's (gsv_stream_create) and the prepared
+ * shapes' side streams.  A prepared notary shape (and the notary partition) forks its chunk roots onto
+ * side streams of its OWN, one per pipeline instance, each a blocking stream on a queue of its own, freed
+ * when the shape is evicted or retired.  Past 8 live side streams a newly prepared shape gets none and
+ * runs its chunk roots after its transactions on the caller's stream (same results; the prepare succeeds). */
+int gsv_ctx_stream_count(gsv_ctx *ctx, int *user_streams, int *side_streams);
 
 /* ---- Keccak-256 (A10) ----
  * Message i is data[off[i] .. off[i+1]); out32[32*i .. +32) = Keccak256(message i). */

@@ -63,3 +63,24 @@ def test_stream_entry_points_reject_null_arguments():
     q = ctypes.c_void_p()
     assert L.gsv_stream_create(None, ctypes.byref(q)) == _lib.E_INVALID_ARG
     assert L.gsv_stream_destroy(None, None) == _lib.E_INVALID_ARG
+    assert L.gsv_ctx_stream_count(None, None, None) == _lib.E_INVALID_ARG
+
+
+def test_stream_cap_is_declared_and_bound():
+    """GSV_MAX_STREAMS in gsv.h is the cap the package enforces (streams owned by the context)"""
+    from gsv import _lib
+    txt = open(os.path.join(ROOT, "include", "gsv.h")).read()
+    assert int(re.search(r"#define GSV_MAX_STREAMS (\d+)", txt).group(1)) == _lib.MAX_STREAMS
+    assert int(re.search(r"#define GSV_ABI_VERSION (\d+)", txt).group(1)) == _lib.load().gsv_abi_version()
+
+
+def test_pipeline_streams_refuses_past_the_cap_before_any_call():
+    """Context.pipeline_streams checks the cap on the Python side first, so a request past it creates
+    nothing (no GPU needed: the check precedes every library call)"""
+    import gsv
+    import pytest
+    from gsv import _lib
+    c = gsv.Context.__new__(gsv.Context)
+    c._h, c.device, c._streams = None, 0, [0] * (_lib.MAX_STREAMS - 1)
+    with pytest.raises(gsv.GsvError):
+        c.pipeline_streams(2)

@@ -328,10 +328,11 @@ def full2(name, doc, terms_of_column, addend=False, dot=False, gen=None):
 def main():
     out = ["// GENERATED by tools/gen_fe9_asm.py — do not edit by hand.",
            "// Column products of secp256k1_fe9.cuh as single inline-asm statements (see the generator's",
-           "// docstring for why).  GSV_FE9_COLS selects the column form: 3 (default) runs the low columns inside",
-           "// the reduction's carry chain (full_lines3), 2 keeps the high columns 9..16 unmasked in fixed",
-           "// register pairs (full_lines2), 1 masks and shifts every column.",
-           "#pragma once", "#include <stdint.h>", "#ifndef GSV_FE9_COLS", "#define GSV_FE9_COLS 3", "#endif",
+           "// docstring for why).  Column form 3: the low columns run inside the reduction's carry chain",
+           "// (full_lines3).  Forms 1 (every column masked and shifted) and 2 (high columns 9..16 unmasked in",
+           "// fixed register pairs) stay in the generator as the instruction emulator's references",
+           "// (tests/test_asm_emulated.py); the kernels use form 3 only (r04: 175 -> 136 instructions a product).",
+           "#pragma once", "#include <stdint.h>",
            "namespace gsv {"]
     specs = [("fe9_mul_full", "r = a * b mod p, weakly normalised (fe9_mul's contract)", MUL_TERMS, False, False),
              ("fe9_sqr_full", "r = a^2 mod p with b = 2a limb-wise (fe9_sqr's contract)", SQR_TERMS, False, False),
@@ -339,16 +340,8 @@ def main():
              ("fe9_sqr_add_full", "r = a^2 + c mod p with b = 2a limb-wise, c limbs < 2^31 (fe9_sqr_add's contract)",
               SQR_TERMS, True, False),
              ("fe9_dot_full", "r = a * b + c * d mod p, one reduction (fe9_dot's contract)", DOT_TERMS, False, True)]
-    out.append("#if GSV_FE9_COLS == 1")
-    for name, doc, terms, add, dot in specs:
-        out += full(name, doc, terms, add, dot)
-    out.append("#elif GSV_FE9_COLS == 2")
-    for name, doc, terms, add, dot in specs:
-        out += full2(name, doc, terms, add, dot)
-    out.append("#else")
     for name, doc, terms, add, dot in specs:
         out += full2(name, doc, terms, add, dot, gen=full_lines3)
-    out.append("#endif")
     out.append("}  // namespace gsv")
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")

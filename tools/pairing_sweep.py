@@ -138,16 +138,9 @@ def main():
     if os.environ.get("SWEEP_PREHEAT"):
         preheat(ctx)
     if os.environ.get("SWEEP_STREAM_SETS"):  # e.g. "0,1,2;3,4,5": pipelines over chosen pool streams
-        if os.environ.get("SWEEP_CUMASK"):  # streams on queues of their own (a CU mask of every CU)
-            import ctypes
-            hip = ctypes.CDLL("libamdhip64.so")
-            cus = torch.cuda.get_device_properties(0).multi_processor_count
-            mask = (ctypes.c_uint32 * ((cus + 31) // 32))(*([0xFFFFFFFF] * ((cus + 31) // 32)))
-            pool = []
-            for _ in range(int(os.environ["SWEEP_CUMASK"])):
-                h = ctypes.c_void_p()
-                assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), len(mask), mask) == 0
-                pool.append(torch.cuda.ExternalStream(h.value))
+        owned = bool(os.environ.get("SWEEP_CUMASK"))
+        if owned:  # streams on queues of their own (gsv_stream_create: a CU mask of every CU), at most 8
+            pool = ctx.pipeline_streams(int(os.environ["SWEEP_CUMASK"]))
         else:
             pool = [torch.cuda.Stream() for _ in range(16)]
         print("pool streams:", " ".join(hex(s_.cuda_stream) for s_ in pool), flush=True)
@@ -156,6 +149,9 @@ def main():
                 ix = [int(x) for x in st.split(",")]
                 dt = run_pipelined(ctx, n, len(ix), streams=[pool[i] for i in ix])
                 print(f"streams {st:>10} checks {n:6d} depth {len(ix)}: {dt * 1e3:8.2f} ms per batch", flush=True)
+        torch.cuda.synchronize()
+        if owned:
+            ctx.destroy_streams(pool)
         return
     if os.environ.get("SWEEP_PIPELINE"):  # e.g. "1,2,3": pipeline depths at auto layout
         for n in sizes:
