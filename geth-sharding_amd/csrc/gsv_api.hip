@@ -161,8 +161,18 @@ constexpr size_t kMaxShapes = 32;
 // side streams on hardware queues of their own, over all of a context's prepared shapes: the hardware
 // scheduler time-slices queues beyond what it maps at once (r05: ~40 leaked queues ran an 8,192-check
 // pairing pipeline at 8.6 instead of 3.8 ms, profiles/r05/ab/pairing_depth_dedicated_leaked_queues.txt);
-// a shape prepared past the bound runs its chains one after the other on the caller's stream
+// a shape prepared past the bound runs its chains one after the other on the caller's stream.
+// GSV_MAX_SIDE_STREAMS (0..8) lowers the bound: 0 = no side streams, every notary step runs its chunk
+// roots after its transactions on one stream (the leg-only profile pass: tools/profile_round.sh, so no
+// dispatch of a traced step overlaps another)
 constexpr int kMaxSideQueues = 8;
+int max_side_queues() {
+    static const int v = [] {
+        const char* e = getenv("GSV_MAX_SIDE_STREAMS");
+        return e ? std::min(std::max(atoi(e), 0), kMaxSideQueues) : kMaxSideQueues;
+    }();
+    return v;
+}
 constexpr size_t kMaxShapeBytes = (size_t)32 << 30;  // of the 288 GB of HBM
 
 }  // namespace
@@ -1073,7 +1083,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
 // are the same and the prepare succeeds (gsv.h).
 int shape_side_init(gsv_ctx* c, Shape& s) {
     if (!s.side.empty()) return GSV_SUCCESS;
-    if (c->side_queues + s.ninst > kMaxSideQueues) return GSV_SUCCESS;  // serial chains
+    if (c->side_queues + s.ninst > max_side_queues()) return GSV_SUCCESS;  // serial chains
     s.side.assign(s.ninst, nullptr);
     s.efork.assign(s.ninst, nullptr);
     s.ejoin.assign(s.ninst, nullptr);

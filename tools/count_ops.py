@@ -5,6 +5,8 @@ tools/build_variant.sh opcount -DGSV_OPCOUNT`), at the bench's batch sizes:
     recovery       one k_ecrecover lane of the configs[1] batch (2^20 signatures)
     pairing_check  one 4-pair check of the configs[4] batch on one GPU (65,536 checks) and of the
                    per-rank batch at N = 8 (8,192 checks: another lane layout, §3.4 of DESIGN.md)
+    notary_tx      one transaction of the configs[3] step (100 shards x 8,192 txs through k_notary_tx:
+                   RLP decode, sighash, recovery, address; every 128th tx invalid by construction)
 
 "mad" is the number of v_mad_u64_u32 (32 x 32 -> 64-bit multiply-adds: the unit of the VALU MAC
 roofline) our kernels execute, from the op counts and each op's mad count in our limb layout:
@@ -86,6 +88,25 @@ def main():
         c["fp_products"] = c.get("bn_mul", 0)
         c["mac_equiv"] = round(W["bn_mul"] * c.get("bn_mul", 0) + W["bn_redc"] * c.get("bn_redc", 0), 1)
         out[name] = c
+    # ---- configs[3]: the notary step's transactions
+    nsh, txs = 100, 8192
+    bodies = torch.empty((nsh * txs * 128,), dtype=torch.uint8, device=dev)
+    exp = torch.empty((nsh * txs,), dtype=torch.uint8, device=dev)
+    ctx.notary_synth_dev(777, 0, nsh, txs, bodies, exp)
+    noff = np.arange(nsh + 1, dtype=np.uint64) * txs * 128
+    ctx.notary_prepare(noff, max_txs=txs)
+    torch.cuda.synchronize()
+    read("notary")  # drop the generator's counts
+    r = torch.empty((nsh, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.empty((nsh,), dtype=torch.int32, device=dev)
+    bm = torch.empty((nsh, txs // 8), dtype=torch.uint8, device=dev)
+    stt = torch.empty((nsh, txs), dtype=torch.uint8, device=dev)
+    ctx.notary_validate_shards_dev(bodies, noff, r, cnt, bm, None, stt, max_txs=txs, prepare=False)
+    torch.cuda.synchronize()
+    assert torch.equal(stt.view(-1), exp)
+    c = per_unit(read("notary"), nsh * txs)
+    c["mac_equiv"] = round(sum(W[k] * c.get(k, 0) for k in ("fe_mul", "fe_sqr", "sc_mul", "sc_sqr", "fe_dot")), 1)
+    out["notary_tx"] = c
     json.dump(out, sys.stdout, indent=1)
     print()
 

@@ -8,12 +8,24 @@ integer VALU instruction counts (SQ_INSTS_VALU_INT32 / _INT64).
 gfx950 correction (MI355X_MICROARCH.md § HBM): FETCH_SIZE counts 64 B per 128-B request for
 wide coalesced reads, so `fetch_bytes_x2` doubles it; which of the two applies depends on the
 kernel's access width — both are reported, with the raw value.
+
+Overlapped dispatches (r06): the counter passes serialise dispatches, but the
+kernel-trace pass does not, so a dispatch that ran beside another in the trace pass (a forked chunk
+root beside k_notary_tx) has a trace duration that is not its own, and any figure dividing its counters
+by that duration is wrong (r05 pmc_notary.json: "clocks" of 0.054 and 5.7 GHz).  Dispatch i of a kernel
+in the trace pass is paired with dispatch i of the same kernel in the SQ pass (the same program issues
+them in the same order); a dispatch whose derived clock, GRBM_GUI_ACTIVE / 8 / its trace duration, lies
+outside [CLK_LO, CLK_HI] GHz is marked overlapped and dropped from every per-dispatch figure.  A kernel
+with no plausible dispatch keeps only its dispatch count and "overlapped_dispatches".
 """
 import json
 import os
 import sqlite3
 import sys
 from collections import defaultdict
+
+
+CLK_LO, CLK_HI = 1.0, 2.6  # GHz: MI355X runs 1.9-2.4 GHz under load (MI355X_MICROARCH.md, DVFS)
 
 
 def short(name):
@@ -35,17 +47,25 @@ def counters(db, names):
 def durations(db):
     con = sqlite3.connect(db)
     d = defaultdict(list)
-    for kname, start, end in con.execute("select name, start, end from kernels"):
+    for kname, start, end in con.execute("select name, start, end from kernels order by start"):
         d[short(kname)].append(end - start)
     return d
 
 
-def per_dispatch(vals):
-    # SQ counters arrive per shader engine: sum per dispatch, then average over dispatches
+def by_dispatch(vals):
+    """per-dispatch sums (SQ counters arrive per shader engine), in dispatch order"""
     agg = defaultdict(float)
     for disp, v in vals:
         agg[disp] += v
-    return sum(agg.values()) / max(len(agg), 1)
+    return [agg[d] for d in sorted(agg)]
+
+
+def per_dispatch(vals, keep=None):
+    """average over the kept dispatches (keep: indices in dispatch order; None = all)"""
+    xs = by_dispatch(vals)
+    if keep is not None:
+        xs = [x for i, x in enumerate(xs) if i in keep]
+    return sum(xs) / max(len(xs), 1)
 
 
 def main(root):
@@ -61,25 +81,35 @@ def main(root):
     for k in sorted(set(dur) | set(fetch)):
         if k.startswith("void at::") or k.startswith("__amd"):
             continue
-        r = {"dispatches": len(dur.get(k, [])),
-             "avg_ms": round(sum(dur[k]) / len(dur[k]) / 1e6, 4) if dur.get(k) else None}
+        s = sq.get(k, {})
+        d = dur.get(k, [])
+        keep = None
+        if s.get("GRBM_GUI_ACTIVE") and d:
+            gui_d = by_dispatch(s["GRBM_GUI_ACTIVE"])
+            n = min(len(gui_d), len(d))
+            keep = {i for i in range(n) if d[i] > 0 and CLK_LO <= gui_d[i] / 8 / d[i] <= CLK_HI}
+        r = {"dispatches": len(d)}
+        if keep is not None and len(keep) < len(d):
+            r["overlapped_dispatches"] = len(d) - len(keep)
+        dk = [x for i, x in enumerate(d) if keep is None or i in keep]
+        r["avg_ms"] = round(sum(dk) / len(dk) / 1e6, 4) if dk else None
+        if keep is not None and not keep:
+            res[k] = r  # no plausible dispatch: nothing derived from an overlapped duration
+            continue
         if "_res" in fetch.get(k, {}):
             vg, ag, scr = fetch[k]["_res"][0][1]
             r.update({"vgpr": vg, "agpr": ag, "scratch_bytes_per_lane": scr})
         if fetch.get(k, {}).get("FETCH_SIZE"):
-            kb = per_dispatch(fetch[k]["FETCH_SIZE"])
+            kb = per_dispatch(fetch[k]["FETCH_SIZE"], keep)
             r["fetch_bytes_raw"] = round(kb * 1024)
             r["fetch_bytes_x2"] = round(kb * 2048)
         if write.get(k, {}).get("WRITE_SIZE"):
-            r["write_bytes"] = round(per_dispatch(write[k]["WRITE_SIZE"]) * 1024)
-        s = sq.get(k, {})
+            r["write_bytes"] = round(per_dispatch(write[k]["WRITE_SIZE"], keep) * 1024)
         if s.get("SQ_INSTS_VALU"):
-            r["sq_insts_valu"] = per_dispatch(s["SQ_INSTS_VALU"])
-            r["sq_waves"] = per_dispatch(s["SQ_WAVES"])
-            busy = per_dispatch(s["SQ_BUSY_CYCLES"]) if s.get("SQ_BUSY_CYCLES") else None
-            act = per_dispatch(s["SQ_ACTIVE_INST_VALU"]) if s.get("SQ_ACTIVE_INST_VALU") else None
-            wcyc = per_dispatch(s["SQ_WAVE_CYCLES"]) if s.get("SQ_WAVE_CYCLES") else None
-            gui = per_dispatch(s["GRBM_GUI_ACTIVE"]) if s.get("GRBM_GUI_ACTIVE") else None
+            r["sq_insts_valu"] = per_dispatch(s["SQ_INSTS_VALU"], keep)
+            r["sq_waves"] = per_dispatch(s["SQ_WAVES"], keep)
+            wcyc = per_dispatch(s["SQ_WAVE_CYCLES"], keep) if s.get("SQ_WAVE_CYCLES") else None
+            gui = per_dispatch(s["GRBM_GUI_ACTIVE"], keep) if s.get("GRBM_GUI_ACTIVE") else None
             if gui:
                 # GRBM_GUI_ACTIVE sums the 8 XCDs' clocks; each of the 1024 SIMDs issues at most one
                 # wave-instruction per cycle: VALU wave-instructions per SIMD per cycle
@@ -96,11 +126,11 @@ def main(root):
                 for key, name in (("SQ_WAIT_ANY", "wait_any_frac"), ("SQ_WAIT_INST_ANY", "wait_inst_any_frac"),
                                   ("SQ_ACTIVE_INST_ANY", "active_inst_any_frac")):
                     if s.get(key):
-                        r[name] = round(per_dispatch(s[key]) / wcyc, 4)
+                        r[name] = round(per_dispatch(s[key], keep) / wcyc, 4)
         i = ints.get(k, {})
         if i.get("SQ_INSTS_VALU_INT32"):
-            r["sq_insts_valu_int32"] = per_dispatch(i["SQ_INSTS_VALU_INT32"])
-            r["sq_insts_valu_int64"] = per_dispatch(i.get("SQ_INSTS_VALU_INT64", []))
+            r["sq_insts_valu_int32"] = per_dispatch(i["SQ_INSTS_VALU_INT32"], keep)
+            r["sq_insts_valu_int64"] = per_dispatch(i.get("SQ_INSTS_VALU_INT64", []), keep)
         res[k] = r
     json.dump(res, sys.stdout, indent=1, sort_keys=True)
     print()

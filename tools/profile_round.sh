@@ -25,6 +25,9 @@ for G in $GROUPS_; do
         continue
     fi
     B="--legs $G --steps 3 --warmup 1 --no-cpu-baseline --pipeline 1 --pairing-pipeline 1 --notary-pipeline 1 --ecrecover-pipeline 1"
+    # the notary step forks its chunk roots beside its transactions: no side streams in the leg-only
+    # passes, so every traced dispatch runs alone (tools/pmc_summary.py drops any that still overlap)
+    if [ $G = notary ]; then export GSV_MAX_SIDE_STREAMS=0; else unset GSV_MAX_SIDE_STREAMS; fi
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -f rocpd csv -d $OUT/$G/trace -o run -- python3 bench.py $B > $OUT/$G.trace.log 2>&1 || { echo "trace pass $G failed"; exit 1; }
     find $OUT/$G/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_$G.csv \;
     # per-dispatch start / end of the library's kernels (small): tools/trace_agreement.py compares the
