@@ -649,6 +649,41 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     ctx.destroy_streams(n_streams)
     k_not, _ = ctx.kernel_time(_lib.K_NOTARY)
     assert int(a_rst.max()) == 0
+    # roofline of the rank's step: the recovery's v_mad_u64_u32 (opcount notary_tx,
+    # per tx) plus the Keccak-f permutations (the chunk roots' PERMS_PER_MIB per 1 MiB body, the sighash
+    # and address of every tx: one each for these <= 135-byte strings), both priced at their VALU peak
+    # and summed as SIMD time; the permutations are converted to MAC-equivalents at the two peaks' ratio
+    oc = opcount("notary_tx")
+    perm_peak = SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / KECCAK_VALU_FLOOR_PER_PERM
+    roof = None
+    if oc:
+        ntx = nloc * NOTARY_TXS
+        perms = nloc * PERMS_PER_MIB + 2 * ntx
+        mac_eq = oc["mac_equiv"] * ntx + perms * PEAK_MAC / perm_peak
+        kt = pmc("gsv::k_notary_tx", "pmc_notary.json")
+        kb = pmc("gsv::k_blob_index", "pmc_notary.json")
+        tx_work = (oc["mac_equiv"] + 2 * PEAK_MAC / perm_peak) * ntx  # what k_notary_tx does
+        roof = {"bound": "valu", "unit": "TMAC/s", "scope": "the rank's whole step (ms_per_step)",
+                "achieved": round(mac_eq / (ndt / nsteps) / 1e12, 3), "peak": round(PEAK_MAC / 1e12, 3),
+                "frac": round(mac_eq / (ndt / nsteps) / PEAK_MAC, 4),
+                "work_per_step": {"txs": ntx, "mac_per_tx": oc["mac_equiv"], "permutations": perms,
+                                  "mac_equiv_per_permutation": round(PEAK_MAC / perm_peak, 1),
+                                  "mac_equiv": round(mac_eq)},
+                "basis": "v_mad_u64_u32 of k_notary_tx (profiles/{R}/opcount.json notary_tx) + Keccak-f "
+                         "permutations at the fixed instruction floor (KECCAK_VALU_FLOOR_PER_PERM), as SIMD "
+                         "time at the 2.4 GHz VALU peaks".format(R=ROUND),
+                "tx_kernels_frac": round(tx_work / (k_not * 1e-3) / PEAK_MAC, 4) if k_not else None,
+                "k_notary_tx": {"profiled_avg_ms": kt.get("avg_ms"),
+                                "frac_profiled_time": round(tx_work / (kt["avg_ms"] * 1e-3) / PEAK_MAC, 4)
+                                if kt.get("avg_ms") and nloc == N_SHARDS else None,
+                                "profiled_clock_ghz": kt.get("profiled_clock_ghz"),
+                                "valu_issue_per_simd_cycle": kt.get("valu_issue_per_simd_cycle"),
+                                "mean_waves_per_simd": kt.get("mean_waves_per_simd"),
+                                "scratch_bytes_per_lane": kt.get("scratch_bytes_per_lane"),
+                                "traffic": pmc_traffic(kt), "write_bytes": kt.get("write_bytes")},
+                "k_blob_index_profiled_avg_ms": kb.get("avg_ms"),
+                "source": "profiles/{R}/pmc_notary.json: leg-only passes with no side streams "
+                          "(GSV_MAX_SIDE_STREAMS=0), overlapped dispatches dropped".format(R=ROUND)}
     out = {"shards_per_s": round(N_SHARDS * nsteps / ndt, 2),
            "txs_per_s": round(N_SHARDS * NOTARY_TXS * nsteps / ndt, 1),
            "shards": N_SHARDS, "txs_per_shard": NOTARY_TXS, "shards_per_rank": per_rank,
@@ -662,7 +697,7 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
            "fixture_configs3": "100 roots + bitmap digest equal tests/golden/configs.json" if fixture_ok
            else "fixture absent",
            "gathered_bytes_per_step": ws * gsv.partition_block_bytes(N_SHARDS, ws, NOTARY_TXS),
-           "scaling": "strong"}
+           "scaling": "strong", "roofline": roof}
     return out, {"nb": nb, "n_exp": n_exp, "n_root": a_root[lo:hi] if nloc else a_root[:0]}
 
 
@@ -1054,7 +1089,7 @@ def main():
                     help="streams (shape instances) consecutive chunk-root batches are spread over")
     ap.add_argument("--pairing-pipeline", type=int, default=0,
                     help="streams (shape instances) consecutive pairing batches are spread over "
-                         "(0 = auto: 4 below 65,536 checks per rank, else 2)")
+                         "(0 = auto: 4 below 65,536 checks per rank, else 1)")
     ap.add_argument("--pairing-checks", type=int, default=0,
                     help="checks per rank in the pairing leg (0 = configs[4]'s 65,536 split over the ranks; "
                          "8192 rehearses a rank of the 8-GPU run on one GPU)")

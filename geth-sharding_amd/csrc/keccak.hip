@@ -84,13 +84,9 @@ __global__ __launch_bounds__(256) void k_keccak256(const uint8_t* __restrict__ d
 hipError_t launch_keccak256(const uint8_t* data, const uint64_t* off, uint32_t n, uint8_t* out32,
                             hipStream_t st) {
     if (n == 0) return hipSuccess;
-    // workgroup size (GSV_KECCAK_BLOCK = 64 / 128 / 256, A/B; the bucket order works within any of them)
-    static const uint32_t blk = [] {
-        const char* e = getenv("GSV_KECCAK_BLOCK");
-        uint32_t b = e ? (uint32_t)atoi(e) : 256u;
-        return (b == 64u || b == 128u) ? b : 256u;
-    }();
-    hipLaunchKernelGGL(k_keccak256, dim3((n + blk - 1) / blk), dim3(blk), 0, st, data, off, n, out32);
+    // 256-thread workgroups: 0.096-0.098 ms per 400 k tx strings against 0.100 (128) and 0.109 (64)
+    // (r05, profiles/r05/ab/keccak_block_depth)
+    hipLaunchKernelGGL(k_keccak256, dim3((n + 255) / 256), dim3(256), 0, st, data, off, n, out32);
     return hipGetLastError();
 }
 

@@ -47,9 +47,9 @@ def _dev_hash(ctx, msgs, shift):
 
 
 @pytest.mark.parametrize("shift", [0, 1, 3, 13])
-def test_keccak256_tx_sized_staged(ctx, oracle, shift):
-    """100-160-byte messages (the bench's tx-string shape): every workgroup's 256 messages fit the LDS
-    staging buffer, so each lane assembles its blocks from LDS; any base alignment."""
+def test_keccak256_tx_sized_any_alignment(ctx, oracle, shift):
+    """100-160-byte messages (the bench's tx-string shape, one or two rate blocks): each lane reads its
+    blocks as aligned dwords realigned with v_alignbyte (keccak.hip load_block), at any base alignment."""
     rng = np.random.default_rng(11 + shift)
     msgs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(100, 161, 1500)]
     out = _dev_hash(ctx, msgs, shift)
@@ -57,18 +57,19 @@ def test_keccak256_tx_sized_staged(ctx, oracle, shift):
         assert bytes(out[i]) == oracle.keccak256(m), i
 
 
-def test_keccak256_staged_and_direct_workgroups(ctx, oracle):
-    """Workgroups whose span exceeds the 36 KiB staging buffer (a long message among them, or many
-    medium ones) read straight from HBM; the others stage.  Spans just below and above the limit, a
-    message crossing the limit, empty messages and a 100 KB message in one batch."""
+def test_keccak256_block_count_buckets_per_workgroup(ctx, oracle):
+    """The kernel takes each 256-message workgroup's messages in block-count order (keccak_dev.cuh
+    wg_bucket_order: buckets 0..7 blocks and 8+, the last one shared by every longer message): one long
+    message among short ones, block counts at and past the last bucket (8 x 136 = 1,088 bytes and up),
+    exact multiples of the rate (the padding block alone), empty messages, a 100 KB message, and a
+    partial last workgroup, at two base alignments."""
     rng = np.random.default_rng(5)
     lens = []
-    lens += list(rng.integers(100, 161, 256))       # wg 0: staged
-    lens += [40000] + list(rng.integers(0, 50, 255))  # wg 1: a long message -> direct
-    lens += [144] * 255 + [36864 - 144 * 255 - 16]    # wg 2: span just below 36 KiB (+ alignment slack)
-    lens += [144] * 255 + [36864 - 144 * 255 + 40]    # wg 3: just above -> direct
-    lens += [0] * 200 + [100000] + [1] * 55           # wg 4: empty messages and one 100 KB message
-    lens += list(rng.integers(130, 140, 300))          # wg 5 + a partial wg 6
+    lens += list(rng.integers(100, 161, 256))                       # wg 0: one or two blocks
+    lens += [40000] + list(rng.integers(0, 50, 255))                # wg 1: one long message
+    lens += [136 * k for k in range(10)] * 25 + [1087, 1088, 1089, 1223, 1224, 1225]  # wg 2: rate multiples
+    lens += [0] * 200 + [100000] + [1] * 55                         # wg 3: empty messages and 100 KB
+    lens += list(rng.integers(130, 140, 300))                       # wg 4 + a partial wg 5
     msgs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in lens]
     for shift in (0, 7):
         out = _dev_hash(ctx, msgs, shift)
