@@ -70,8 +70,9 @@ if os.environ.get("SWEEP_CASES"):  # e.g. "4,,1;2,,1" = k,final3,miller2 (empty 
 _STREAMS = []
 
 
-def run_pipelined(ctx, n, depth, steps=12, streams=None):
+def run_pipelined(ctx, n, depth, steps=None, streams=None):
     """n checks per batch, consecutive batches over `depth` streams (gsv_ctx_set_pipeline_depth)"""
+    steps = steps or int(os.environ.get("SWEEP_STEPS", "12"))
     if not os.environ.get("SWEEP_KEEP_LAYOUT"):  # else the GSV_BN_* overrides in the environment apply
         for v in ("GSV_BN_PAIRS_PER_LANE", "GSV_BN_FINAL3", "GSV_BN_MILLER2"):
             os.environ.pop(v, None)
