@@ -902,11 +902,12 @@ def leg_pairing(ctx, stream, dev, ws, rank, args):
     stream.synchronize()
     # consecutive batches on `depth` streams with their own shape instances (as the chunk-root leg):
     # one batch's latency-bound Miller / final-exponentiation waves share the SIMDs with the next
-    # batch's kernels.  auto (r05, streams on queues of their own, profiles/r05/ab/pairing_depth_dedicated.txt):
-    # four batches in flight below 65,536 checks (8,192: 6.47 / 4.53 / 3.76 / 3.67 ms per batch at depth
-    # 1-4; 16,384: 7.72 / 6.98 / 6.26 / 6.23), one at 65,536 and up, where every kernel alone fills the
-    # GPU and overlapping batches only contend (19.56 / 20.57 / 20.56 / 20.20 ms)
-    depth = args.pairing_pipeline if args.pairing_pipeline > 0 else (4 if nloc < 65536 else 1)
+    # batch's kernels.  auto: one at 65,536 checks and up, where every kernel alone fills the GPU and
+    # overlapping batches only contend (r05, streams on queues of their own: 19.56 / 20.57 / 20.56 /
+    # 20.20 ms per batch at depth 1-4, profiles/r05/ab/pairing_depth_dedicated.txt); six below, where
+    # the library then takes the work-efficient layout (k = 4, one-lane final: 8,192 checks 3.13 ms per
+    # batch against 3.30 at r05's depth 4, r06, profiles/r06/ab/pairing_rank_depth.txt)
+    depth = args.pairing_pipeline if args.pairing_pipeline > 0 else (6 if nloc < 65536 else 1)
     ctx.set_pipeline_depth(depth)
     streams = pipeline_streams(ctx, depth, stream, dev)  # on queues of their own (as the chunk-root leg)
     pvk = [pver] + [torch.empty_like(pver) for _ in range(depth - 1)]
@@ -1089,7 +1090,7 @@ def main():
                     help="streams (shape instances) consecutive chunk-root batches are spread over")
     ap.add_argument("--pairing-pipeline", type=int, default=0,
                     help="streams (shape instances) consecutive pairing batches are spread over "
-                         "(0 = auto: 4 below 65,536 checks per rank, else 1)")
+                         "(0 = auto: 6 below 65,536 checks per rank, else 1)")
     ap.add_argument("--pairing-checks", type=int, default=0,
                     help="checks per rank in the pairing leg (0 = configs[4]'s 65,536 split over the ranks; "
                          "8192 rehearses a rank of the 8-GPU run on one GPU)")

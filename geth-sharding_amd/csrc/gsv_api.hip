@@ -92,7 +92,7 @@ struct Shape {
     size_t o_src = 0, o_pidx = 0, o_lfirst = 0, o_clane = 0, o_cbad = 0, o_pstat = 0, o_lines = 0,
            o_lstat = 0, o_fv = 0, o_fws = 0;
     uint32_t maxl = 1;  // the most Miller lanes of any check
-    bool deep = false;  // laid out for three or more batches in flight (pairing_shape's depth >= 3)
+    int deep = 0;  // pairing layout class of the depth it was prepared at (bn_depth_class)
     // per instance, the side stream and fork/join events of a shape that runs two launch chains at
     // once (the notary's chunk roots; the pairing's concurrent layout), created at prepare
     std::vector<hipStream_t> side;
@@ -908,9 +908,17 @@ int chunk_shape(gsv_ctx* c, Shape& s, const uint64_t* start, const uint64_t* end
 // Final exponentiation layout: one lane per check is a ~10^4-product dependent chain; when the batch
 // gives the SIMDs fewer than one such wave each, three lanes per check share its exponentiations by
 // u (a third of the chain).  GSV_BN_FINAL3 = 0/1 forces the choice (A/B timing).
-bool bn_final3(size_t nchecks, int cus) {
+// From BN_DEEP batches in flight the other batches fill what one small batch leaves idle even at k = 4
+// pairs per Miller lane and one lane per check in the final exponentiation (the layout with the fewest
+// products): 8,192 checks 3.13 ms per batch at depth 6 against 3.30 for the depth-3 rule's k = 2 /
+// three-lane final at depth 4 (r06, profiles/r06/ab/pairing_rank_depth.txt; k = 4 at depth 4: 3.86).
+constexpr int BN_DEEP = 6;
+// the depth classes whose pairing layouts differ: 1-2, 3-5 (bn_pairs_per_lane's sixth-of-a-wave
+// target, no two-lane Miller), 6 and up
+int bn_depth_class(int depth) { return depth >= BN_DEEP ? 2 : depth >= 3 ? 1 : 0; }
+bool bn_final3(size_t nchecks, int cus, int depth) {
     if (const char* e = getenv("GSV_BN_FINAL3")) return atoi(e) != 0;
-    return nchecks < (size_t)std::max(cus, 1) * 4 * 64;
+    return depth < BN_DEEP && nchecks < (size_t)std::max(cus, 1) * 4 * 64;
 }
 // Two lanes per Miller lane while twice the Miller lanes still fit one wave per SIMD (the Miller
 // kernel's register budget admits one wave per SIMD).  GSV_BN_MILLER2 = 0/1 forces the choice.
@@ -958,6 +966,7 @@ uint32_t bn_pairs_per_lane(size_t np, int cus, int depth) {
         int k = atoi(e);
         if (k >= 1) return (uint32_t)k;
     }
+    if (depth >= BN_DEEP) return 4;  // six or more batches in flight: the most work-efficient layout
     const size_t waves = bn_miller_w2() ? 2 : 1;  // Miller waves per SIMD the kernel's registers admit
     size_t target = (size_t)std::max(cus, 1) * 4 * 64 * waves / (depth >= 3 ? 6 : 1);
     for (uint32_t k = 4; k > 1; k >>= 1)
@@ -1046,8 +1055,8 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     s.np = np;
     s.nl = lane_first.size() - 1;
     s.nchecks = n;
-    s.deep = depth >= 3;
-    s.layout = (bn_final3(n, cus) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
+    s.deep = bn_depth_class(depth);
+    s.layout = (bn_final3(n, cus, depth) ? gsv::GSV_BN_LAYOUT_FINAL3 : 0) |
                (bn_miller2(s.nl, cus, depth) ? gsv::GSV_BN_LAYOUT_MILLER2 : 0) |
                (bn_miller_w2() ? gsv::GSV_BN_LAYOUT_MILLERW2 : 0) |
                (bn_lines_w2(np, cus) ? gsv::GSV_BN_LAYOUT_LINESW2 : 0) | (bn_miller_l() ? gsv::GSV_BN_LAYOUT_MILLERL : 0);
@@ -1406,7 +1415,7 @@ int shape_get(gsv_ctx* c, uint64_t kind, std::vector<uint64_t>&& key, B&& build,
     Shape* s = shape_find(c, kind, key);
     // a pairing shape's layout depends on the depth class it was prepared at (three or more batches in
     // flight pick the work-efficient layout, pairing_shape): a prepare at the other class rebuilds it
-    const bool reclass = s && kind == SK_PAIRING && s->deep != (c->pipeline_depth >= 3);
+    const bool reclass = s && kind == SK_PAIRING && s->deep != bn_depth_class(c->pipeline_depth);
     if (s && (s->ninst < c->pipeline_depth || reclass)) {
         // prepared before the depth was raised (or at the other depth class): build a new one, and
         // RETIRE the old one instead of freeing it (it is never found again but keeps its memory until

@@ -161,6 +161,42 @@ def test_configs4_rank_batch_depth_three(ctx, monkeypatch, layout):
         assert (got == e).all(), [(i, int(got[i]), int(e[i])) for i in np.nonzero(got != e)[0][:10]]
 
 
+@pytest.mark.parametrize("depth", [4, 6])
+def test_configs4_rank_batch_dedicated_queues(ctx, depth):
+    """The N = 8 per-rank share of configs[4] (8,192 checks, seed 5000, all six seeded classes) exactly as
+    bench.py runs it: prepared at the pipeline depth, 2 x depth batches over `depth` streams from
+    gsv_stream_create (hardware queues of their own), auto layout — the depth-3 rule's k = 2 / three-lane
+    final at depth 4, the deep rule's k = 4 / one-lane final at depth 6 (r06).  Every batch's verdicts
+    equal the generator's expectation."""
+    import torch
+    n = 8192
+    dev = torch.device("cuda", ctx.device)
+    pin = torch.empty((n, 768), dtype=torch.uint8, device=dev)
+    exp = torch.empty((n,), dtype=torch.uint8, device=dev)
+    ctx.bn256_synth_checks_dev(5000, pin, exp)
+    torch.cuda.synchronize()
+    off = np.arange(n + 1, dtype=np.uint64) * 768
+    ctx.set_pipeline_depth(depth)
+    try:
+        ctx.pairing_prepare(off)
+    finally:
+        ctx.set_pipeline_depth(1)
+    ss = ctx.pipeline_streams(depth)
+    try:
+        outs = [torch.full((n,), 9, dtype=torch.uint8, device=dev) for _ in range(2 * depth)]
+        torch.cuda.synchronize()
+        for i, o in enumerate(outs):
+            ctx.pairing_check_batch_dev(pin, off, o, stream=ss[i % depth], prepare=False)
+        for s_ in ss:
+            s_.synchronize()
+    finally:
+        ctx.destroy_streams(ss)
+    e = exp.cpu().numpy()
+    for o in outs:
+        got = o.cpu().numpy()
+        assert (got == e).all(), [(i, int(got[i]), int(e[i])) for i in np.nonzero(got != e)[0][:10]]
+
+
 @pytest.mark.parametrize("k,miller2", [(1, "0"), (1, "1"), (2, "0"), (2, "1")])
 def test_pairing_two_lane_miller_on_off(ctx, oracle, monkeypatch, k, miller2):
     """The two-lane Miller step (small batches at pipeline depth <= 2) and the one-lane loop (what a

@@ -61,9 +61,9 @@ def test_overlapped_dispatches_are_dropped(tmp_path):
         pmc_summary.main(root)
     d = json.loads(buf.getvalue())
     a, b = d["gsv::k_a"], d["gsv::k_b"]
-    assert a["dispatches"] == 3 and a["overlapped_dispatches"] == 1
+    assert a["dispatches"] == 3 and a["implausible_clock_dispatches"] == 1
     assert a["avg_ms"] == 1.0                          # the 20 ms overlapped duration is not averaged in
     assert a["profiled_clock_ghz"] == 2.0
     assert a["fetch_bytes_raw"] == 100 * 1024          # the overlapped dispatch's counters are dropped too
-    assert b["dispatches"] == 1 and b["overlapped_dispatches"] == 1
+    assert b["dispatches"] == 1 and b["implausible_clock_dispatches"] == 1
     assert b["avg_ms"] is None and "profiled_clock_ghz" not in b and "fetch_bytes_raw" not in b

@@ -15,8 +15,10 @@ root beside k_notary_tx) has a trace duration that is not its own, and any figur
 by that duration is wrong (r05 pmc_notary.json: "clocks" of 0.054 and 5.7 GHz).  Dispatch i of a kernel
 in the trace pass is paired with dispatch i of the same kernel in the SQ pass (the same program issues
 them in the same order); a dispatch whose derived clock, GRBM_GUI_ACTIVE / 8 / its trace duration, lies
-outside [CLK_LO, CLK_HI] GHz is marked overlapped and dropped from every per-dispatch figure.  A kernel
-with no plausible dispatch keeps only its dispatch count and "overlapped_dispatches".
+outside [CLK_LO, CLK_HI] GHz is dropped from every per-dispatch figure and counted in
+"implausible_clock_dispatches" (an overlapped dispatch, or one too short for its counter window: a
+~0.1 ms launch's GRBM_GUI_ACTIVE window includes the dispatch overhead).  A kernel with no plausible
+dispatch keeps only its dispatch count and that count.
 """
 import json
 import os
@@ -90,7 +92,7 @@ def main(root):
             keep = {i for i in range(n) if d[i] > 0 and CLK_LO <= gui_d[i] / 8 / d[i] <= CLK_HI}
         r = {"dispatches": len(d)}
         if keep is not None and len(keep) < len(d):
-            r["overlapped_dispatches"] = len(d) - len(keep)
+            r["implausible_clock_dispatches"] = len(d) - len(keep)
         dk = [x for i, x in enumerate(d) if keep is None or i in keep]
         r["avg_ms"] = round(sum(dk) / len(dk) / 1e6, 4) if dk else None
         if keep is not None and not keep:
