@@ -81,7 +81,7 @@ VALU_ISSUE_PEAK = 0.5
 PEAK_LANE_OPS = SIMDS * 64 * VALU_ISSUE_PEAK * CLOCK          # 7.86e13 full-rate 32-bit lane-ops/s
 PEAK_MAC = SIMDS * 16 * CLOCK                                 # 3.93e13 v_mad_u64_u32 lane-ops/s
 HBM_PEAK_GBPS = 8000.0
-ROUND = "r05"
+ROUND = "r06"
 PROFILES = os.path.join(ROOT, "profiles", ROUND)
 LEGS = ["ecrecover", "chunk_root", "notary", "keccak", "tx_root", "poc", "headers", "pairing"]
 
@@ -364,9 +364,11 @@ def leg_ecrecover(ctx, stream, dev, ws, rank, args):
         ctx.synth_sign_dev(1000 + rank, msg, sig, epub, eaddr, stream=stream)
     stream.synchronize()
 
-    # --ecrecover-pipeline D > 1: consecutive batches on D streams with hardware queues of their own,
-    # each with its own outputs (the recovery keeps no per-call state), so one batch's last wave round
-    # overlaps the next batch's first (+1.2-1.6 % in a standalone A/B, profiles/r05/ab/ecrecover_steps.txt)
+    # --ecrecover-pipeline D > 1 (2 by default since r06): consecutive batches on D streams with hardware
+    # queues of their own, each with its own outputs (the recovery keeps no per-call state), so one
+    # batch's last wave round overlaps the next batch's first (+1.2-1.6 % in a standalone A/B,
+    # profiles/r05/ab/ecrecover_steps.txt, ecrecover_depth_live_events.txt): a node validating a stream
+    # of transaction batches runs them so, as the chunk-root, notary and pairing legs do
     edepth = max(1, args.ecrecover_pipeline)
     estreams = pipeline_streams(ctx, edepth, stream, dev)
     eouts = [(pub, addr, st)] + [(torch.empty_like(pub), torch.empty_like(addr), torch.empty_like(st))
@@ -1083,9 +1085,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--legs", default=",".join(LEGS), help="comma list of " + ",".join(LEGS))
-    ap.add_argument("--ecrecover-pipeline", type=int, default=1,
-                    help="streams consecutive ecrecover batches are spread over (1, the default: one stream, "
-                         "with the roofline's kernel time from HIP events over the timed region itself)")
+    ap.add_argument("--ecrecover-pipeline", type=int, default=2,
+                    help="streams consecutive ecrecover batches are spread over (2, the default since r06: two "
+                         "batches in flight on dedicated-queue streams, as the other legs; the roofline's "
+                         "kernel time then comes from a separate single-stream instrumented pass; 1: one "
+                         "stream, kernel time from HIP events over the timed region itself)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="streams (shape instances) consecutive chunk-root batches are spread over")
     ap.add_argument("--pairing-pipeline", type=int, default=0,
