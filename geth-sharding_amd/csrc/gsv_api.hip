@@ -1422,7 +1422,9 @@ int shape_get(gsv_ctx* c, uint64_t kind, std::vector<uint64_t>&& key, B&& build,
         // LRU eviction, which drains its queued work first), so a graph captured from it stays valid.
         // Its side streams go now (a captured graph holds no streams): the new shape needs the queues.
         s->kind |= 1ull << 63;
-        s->release_side();
+        bool cap = false;  // a capture still open on a side stream keeps it until eviction
+        for (hipStream_t q : s->side) cap = cap || (q && capturing(q));
+        if (!cap) s->release_side();
         s = nullptr;
     }
     if (!s) {
