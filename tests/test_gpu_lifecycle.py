@@ -217,3 +217,58 @@ def test_capture_beside_uncaptured_calls_of_other_shapes(ctx):
     for a, b in zip(got, ea):
         assert torch.equal(a, b)
     assert (got[1].cpu().numpy() == txs).all()
+
+
+_CHILD_NO_SIDE = textwrap.dedent("""
+    import os, sys
+    sys.path.insert(0, os.path.join(sys.argv[1], "geth-sharding_amd"))
+    import numpy as np
+    import torch
+    import gsv
+    ctx = gsv.default_context()
+    nsh, txs = 3, 256
+    bodies = torch.empty(nsh * txs * 128, dtype=torch.uint8, device="cuda")
+    exp = torch.empty(nsh * txs, dtype=torch.uint8, device="cuda")
+    ctx.notary_synth_dev(44, 0, nsh, txs, bodies, exp)
+    torch.cuda.synchronize()
+    off = np.arange(nsh + 1, dtype=np.uint64) * txs * 128
+    ctx.set_pipeline_depth(3)
+    ctx.notary_prepare(off, max_txs=txs)
+    ctx.set_pipeline_depth(1)
+    assert ctx.stream_count() == (0, 0), ctx.stream_count()
+    ss = ctx.pipeline_streams(3)
+    outs = []
+    for i in range(6):
+        o = [torch.zeros((nsh, 32), dtype=torch.uint8, device="cuda"), torch.zeros((nsh,), dtype=torch.int32, device="cuda"),
+             torch.zeros((nsh, txs // 8), dtype=torch.uint8, device="cuda"), torch.zeros((nsh, txs), dtype=torch.uint8, device="cuda")]
+        ctx.notary_validate_shards_dev(bodies, off, o[0], o[1], o[2], None, o[3], max_txs=txs, stream=ss[i % 3],
+                                       prepare=False)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o[3].view(-1), exp) and (o[1].cpu().numpy() == txs).all()
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[2], outs[0][2])
+    print("roots", outs[0][0].cpu().numpy().tobytes().hex(), flush=True)
+""")
+
+
+def test_no_side_streams_runs_the_chunk_roots_serially(ctx):
+    """GSV_MAX_SIDE_STREAMS=0 (the leg-only profile pass, tools/profile_round.sh): a notary shape gets no
+    side streams, its steps run the chunk roots after the transactions on the caller's stream, six
+    pipelined steps give the construction's statuses, and the roots equal this process's (forked) ones."""
+    import torch
+    env = dict(os.environ, GSV_MAX_SIDE_STREAMS="0")
+    p = subprocess.run([sys.executable, "-c", _CHILD_NO_SIDE, ROOT], capture_output=True, text=True, timeout=240,
+                       env=env)
+    assert p.returncode == 0, f"rc {p.returncode}\nstdout:\n{p.stdout[-2000:]}\nstderr:\n{p.stderr[-4000:]}"
+    roots = [l.split()[1] for l in p.stdout.splitlines() if l.startswith("roots ")][0]
+    nsh, txs = 3, 256
+    bodies = torch.empty(nsh * txs * 128, dtype=torch.uint8, device="cuda")
+    ctx.notary_synth_dev(44, 0, nsh, txs, bodies)
+    torch.cuda.synchronize()
+    off = np.arange(nsh + 1, dtype=np.uint64) * txs * 128
+    o = [torch.zeros((nsh, 32), dtype=torch.uint8, device="cuda"), torch.zeros((nsh,), dtype=torch.int32, device="cuda"),
+         torch.zeros((nsh, txs // 8), dtype=torch.uint8, device="cuda")]
+    ctx.notary_validate_shards_dev(bodies, off, o[0], o[1], o[2], None, None, max_txs=txs)
+    torch.cuda.synchronize()
+    assert o[0].cpu().numpy().tobytes().hex() == roots
