@@ -626,8 +626,9 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     # times the steps and the timed region spans about the same wall time at every N.  A pipeline's
     # fill and drain cost about one step's latency (~1.3 ms at 13 shards) per timed region: 12 timed
     # 13-shard steps read 1.28 ms per step, 40 read 1.16 (the steady state; 100 shards 8.76 ms, i.e.
-    # 98 % of linear), profiles/r06/ab/notary_stagger_steps.txt
-    nsteps = max(2 * depth, args.steps // 2) * ws
+    # 98 % of linear), profiles/r06/ab/notary_stagger_steps.txt.  --steps of them per rank at N = 1 (r05:
+    # --steps / 2), as the ecrecover and chunk-root legs
+    nsteps = max(2 * depth, args.steps) * ws
     for i in range(1, max(depth, args.warmup)):  # warm the other instances (at least --warmup steps)
         notary_step(i=i)
     for s_ in n_streams:
