@@ -94,7 +94,7 @@ struct Shape {
     uint32_t maxl = 1;  // the most Miller lanes of any check
     int deep = 0;  // pairing layout class of the depth it was prepared at (bn_depth_class)
     // per instance, the side stream and fork/join events of a shape that runs two launch chains at
-    // once (the notary's chunk roots; the pairing's concurrent layout), created at prepare
+    // once (the notary's chunk roots beside its transactions), created at prepare
     std::vector<hipStream_t> side;
     std::vector<hipEvent_t> efork, ejoin;
     bool side_borrowed = false;  // host-path shape: the context's side stream and events, not its own
@@ -1084,7 +1084,7 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
     return GSV_SUCCESS;
 }
 // a side stream and fork/join events per instance (at prepare), for shapes that run two independent
-// launch chains at once: the notary's chunk roots (and the pairing's concurrent layout).  The streams are
+// launch chains at once: the notary's chunk roots beside its transactions.  The streams are
 // the SHAPE's own, on hardware queues of their own (a context-wide pool let an uncaptured call
 // of one shape enqueue onto a side stream another shape's capture had joined); they live until the shape
 // is evicted or retired.  Past kMaxSideQueues live side queues, or when HIP refuses a stream or event, the

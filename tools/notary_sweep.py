@@ -45,7 +45,9 @@ def main():
             torch.cuda.synchronize()
             for r, c, b, s in outs:
                 assert torch.equal(s.view(-1), exp), "statuses differ from the construction"
-            steps = int(os.environ.get("NOTARY_STEPS", "12"))
+            # 40 timed steps (r06; 12 through r05): a pipeline's fill and drain cost about one step's
+            # latency per measurement, 0.1 ms per 13-shard step at 12 steps (profiles/r06/ab/notary_stagger_steps.txt)
+            steps = int(os.environ.get("NOTARY_STEPS", "40"))
             t0 = time.perf_counter()
             for i in range(steps):
                 r, c, b, _ = outs[i % depth]
