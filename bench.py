@@ -1100,10 +1100,12 @@ def main():
     ap.add_argument("--pairing-checks", type=int, default=0,
                     help="checks per rank in the pairing leg (0 = configs[4]'s 65,536 split over the ranks; "
                          "8192 rehearses a rank of the 8-GPU run on one GPU)")
-    ap.add_argument("--notary-pipeline", type=int, default=3,
+    ap.add_argument("--notary-pipeline", type=int, default=4,
                     help="streams (shape instances) consecutive notary partition steps are spread over "
                          "(r05, queues of their own: 1 / 2 / 3 deep 10,560 / 11,457 / 11,623 shards/s, "
-                         "profiles/r05/ab/chunk_notary_depth.txt)")
+                         "profiles/r05/ab/chunk_notary_depth.txt; r06: 4 since the N = 8 share of 13 shards "
+                         "reads 1.125 ms per step four deep against 1.16-1.20 three deep, 100 shards equal at "
+                         "2-4, profiles/r06/ab/notary_share_depths.txt)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rank plumbing only (no GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -1087,12 +1087,25 @@ int pairing_shape(gsv_ctx* c, Shape& s, const uint64_t* off, size_t n, Layout& L
 // launch chains at once: the notary's chunk roots beside its transactions.  The streams are
 // the SHAPE's own, on hardware queues of their own (a context-wide pool let an uncaptured call
 // of one shape enqueue onto a side stream another shape's capture had joined); they live until the shape
-// is evicted or retired.  Past kMaxSideQueues live side queues, or when HIP refuses a stream or event, the
-// shape gets no side streams and runs its chains one after the other on the caller's stream: the results
-// are the same and the prepare succeeds (gsv.h).
+// is evicted or retired.  Past kMaxSideQueues live side queues the shape being prepared takes them from
+// the least recently used shapes that hold some (those then run their chains one after the other until
+// they are prepared again: r06, a sweep over shard counts had left a 13-shard shape holding six queues
+// and the next 25-shard shape ran serially, 2.74 instead of 2.15 ms per step).  When that is not enough
+// (a capture still open on every candidate's side stream), or HIP refuses a stream or event, the shape
+// gets no side streams and runs its chains one after the other on the caller's stream: the results are
+// the same and the prepare succeeds (gsv.h).
 int shape_side_init(gsv_ctx* c, Shape& s) {
     if (!s.side.empty()) return GSV_SUCCESS;
-    if (c->side_queues + s.ninst > max_side_queues()) return GSV_SUCCESS;  // serial chains
+    const int cap = max_side_queues();
+    if (s.ninst > cap) return GSV_SUCCESS;  // serial chains
+    for (auto it = c->shapes.rbegin(); it != c->shapes.rend() && c->side_queues + s.ninst > cap; ++it) {
+        Shape* v = it->get();
+        if (v == &s || v->side.empty() || v->side_borrowed) continue;
+        bool open = false;  // a graph being captured through v's side streams keeps them
+        for (hipStream_t q : v->side) open = open || (q && capturing(q));
+        if (!open) v->release_side();
+    }
+    if (c->side_queues + s.ninst > cap) return GSV_SUCCESS;  // serial chains
     s.side.assign(s.ninst, nullptr);
     s.efork.assign(s.ninst, nullptr);
     s.ejoin.assign(s.ninst, nullptr);

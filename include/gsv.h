@@ -157,8 +157,10 @@ int gsv_stream_destroy(gsv_ctx *ctx, void *stream);
 /* Live dedicated-queue streams of the context: the caller's (gsv_stream_create) and the prepared
  * shapes' side streams.  A prepared notary shape (and the notary partition) forks its chunk roots onto
  * side streams of its OWN, one per pipeline instance, each a blocking stream on a queue of its own, freed
- * when the shape is evicted or retired.  Past 8 live side streams a newly prepared shape gets none and
- * runs its chunk roots after its transactions on the caller's stream (same results; the prepare succeeds). */
+ * when the shape is evicted or retired.  At most 8 side streams are live per context: a prepare past
+ * that takes them from the least recently used shapes holding some, which then run their chunk roots
+ * after their transactions on the caller's stream until prepared again (same results; the prepare
+ * succeeds; a shape whose side stream has a graph capture open keeps it). */
 int gsv_ctx_stream_count(gsv_ctx *ctx, int *user_streams, int *side_streams);
 
 /* ---- Keccak-256 (A10) ----

@@ -125,8 +125,9 @@ def _notary_outs(torch, dev, nsh, txs):
 
 def test_side_streams_are_per_shape_and_bounded():
     """Each prepared notary shape owns one side stream per pipeline instance; a retired shape gives its
-    side streams back; past 8 live side streams a new shape runs its chunk roots on the caller's stream,
-    with the same results."""
+    side streams back; past 8 live side streams a newly prepared shape takes the least recently used
+    shape's (which then runs its chunk roots after its transactions on the caller's stream); every shape
+    gives the same results as a fresh context's."""
     import torch
     import gsv
     c = gsv.Context(0)
@@ -147,7 +148,7 @@ def test_side_streams_are_per_shape_and_bounded():
         assert c.stream_count()[1] == 4
         c.notary_prepare(cases[1][2], max_txs=txs)
         assert c.stream_count()[1] == 8
-        c.notary_prepare(cases[2][2], max_txs=txs)  # past the bound: no side streams, prepare succeeds
+        c.notary_prepare(cases[2][2], max_txs=txs)  # past the bound: takes the LRU shape's (case 0's) four
         assert c.stream_count()[1] == 8
         c.set_pipeline_depth(1)
         ref = gsv.default_context()
