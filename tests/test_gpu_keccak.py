@@ -91,3 +91,53 @@ def test_keccak256_large_ragged_vs_oracle(ctx, oracle):
     out = ctx.keccak256_batch(msgs)
     bad = [i for i, m in enumerate(msgs) if bytes(out[i]) != oracle.keccak256(m)]
     assert not bad, bad[:10]
+
+
+def test_keccak256_tail_block_reads_at_batch_end(ctx, oracle):
+    """The final block is read as whole 16-byte groups (keccak.hip load_block_tail) when at least 16
+    bytes of the batch follow the message; the bytes read past it (the next messages) are masked.  A wave
+    holding a message that ends within 16 bytes of the batch's end reads dword by dword instead.  Here
+    the batch ends on a 4 KB boundary of its allocation with 0xff bytes after it, and its last messages
+    are 0-17 bytes long; the batch starts at every alignment 0-3."""
+    import torch
+    for shift in range(4):
+        rng = np.random.default_rng(77)
+        lens = [100 + shift] + list(rng.integers(100, 161, 700)) + list(range(18)) + [0, 0, 5]
+        msgs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in lens]
+        flat = np.frombuffer(b"".join(msgs), np.uint8).copy()
+        off = np.zeros(len(msgs) + 1, np.int64)
+        off[1:] = np.cumsum(lens)
+        buf = torch.full((len(flat) + 3 * 4096,), 0xff, dtype=torch.uint8, device="cuda")
+        end = ((buf.data_ptr() + len(flat) + 4096) // 4096) * 4096 - buf.data_ptr()  # page-aligned end
+        start = end - len(flat)
+        assert 0 <= start and end + 16 <= buf.numel()
+        buf[start:end] = torch.from_numpy(flat).cuda()
+        out = torch.empty((len(msgs), 32), dtype=torch.uint8, device="cuda")
+        ctx.keccak256_batch_dev(buf[start:end], torch.from_numpy(off).cuda(), out)
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        bad = [i for i, m in enumerate(msgs) if bytes(o[i]) != oracle.keccak256(m)]
+        assert not bad, ((buf.data_ptr() + start) % 4, bad[:10])
+
+
+@pytest.mark.parametrize("out_shift", [1, 4, 8])
+def test_keccak256_unaligned_digest_output(ctx, oracle, out_shift):
+    """Digests to an output buffer that is not 16-byte aligned (the kernels store two dwordx4 only when it
+    is, bytes otherwise), across whole workgroups of messages with one to three rate blocks."""
+    import torch
+    rng = np.random.default_rng(31 + out_shift)
+    lens = rng.integers(0, 400, 1300)
+    msgs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in lens]
+    flat = np.frombuffer(b"".join(msgs), np.uint8).copy()
+    off = np.zeros(len(msgs) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    data = torch.zeros(len(flat) + 64, dtype=torch.uint8, device="cuda")
+    data[:len(flat)] = torch.from_numpy(flat).cuda()
+    big = torch.full((len(msgs) * 32 + 32,), 0xee, dtype=torch.uint8, device="cuda")
+    out = big[out_shift:out_shift + len(msgs) * 32].view(len(msgs), 32)
+    ctx.keccak256_batch_dev(data, torch.from_numpy(off).cuda(), out)
+    torch.cuda.synchronize()
+    o = big.cpu().numpy()
+    assert (o[:out_shift] == 0xee).all() and (o[out_shift + len(msgs) * 32:] == 0xee).all()
+    bad = [i for i, m in enumerate(msgs) if bytes(o[out_shift + 32 * i:out_shift + 32 * i + 32]) != oracle.keccak256(m)]
+    assert not bad, bad[:10]
