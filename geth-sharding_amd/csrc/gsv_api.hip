@@ -1157,13 +1157,14 @@ int notary_shape(gsv_ctx* c, Shape& s, const uint64_t* start, const uint64_t* en
     if (cidlen > 64) return GSV_E_INVALID_ARG;
     for (size_t i = 0; i < n; i++)
         if (end[i] < start[i] || end[i] - start[i] > MAX_BODY) return GSV_E_TOO_LARGE;
-    // chain-id buffers: 64-byte big-endian value and the sighash suffix rlp(chainId) || 0x80 0x80
+    // chain-id buffers: 64-byte big-endian value at 0 and the sighash suffix rlp(chainId) || 0x80 0x80
+    // (<= 67 bytes) at 128, zero bytes around it (k_notary_tx reads it as aligned dwords)
     uint8_t host[256] = {0};
     if (cidlen) memcpy(host + 64 - cidlen, cid, cidlen);
     size_t z = 0;
     while (z < cidlen && cid[z] == 0) z++;
     size_t cn = cidlen - z, sl = 0;
-    uint8_t* suf = host + 64;
+    uint8_t* suf = host + 128;
     if (cn == 1 && cid[z] < 0x80) suf[sl++] = cid[z];
     else {
         suf[sl++] = (uint8_t)(0x80 + cn);
@@ -1220,7 +1221,7 @@ int notary_run(gsv_ctx* c, const Shape& s, size_t n, const uint8_t* d_bodies, ui
     HIPCHK(gsv::launch_blob_index(d_bodies, s.at<uint64_t>(s.o_noff), s.at<uint32_t>(s.o_nlen), (uint32_t)n,
                                   s.max_txs, s.at<void>(s.o_blobs), d_cnt, st));
     HIPCHK(gsv::launch_notary_tx(d_bodies, s.at<uint64_t>(s.o_noff), s.at<void>(s.o_blobs), d_cnt, (uint32_t)n,
-                                 s.max_txs, s.at<uint8_t>(s.o_cid), s.at<uint8_t>(s.o_cid) + 64, s.sfx_len,
+                                 s.max_txs, s.at<uint8_t>(s.o_cid), s.at<uint8_t>(s.o_cid) + 128, s.sfx_len,
                                  s.signer_kind, c->gtab, d_bitmap, (uint32_t)bm, d_senders, d_status, st));
     hook_end(c, GSV_K_NOTARY);
     if (fork) {

@@ -85,11 +85,32 @@ __global__ __launch_bounds__(BI_THREADS) void k_blob_index(const uint8_t* __rest
 // Measured and not kept (r05): staging each wave's chunk span in its columns of the GLV table's LDS rows
 // (free until recover_core builds the table) and decoding from LDS instead of single-byte global loads:
 // tx kernels 8.45-8.66 vs 8.60-8.67 ms per configs[3] step (profiles/r05/ab/recover_ab_*.json), within
-// noise.  The per-tx gap to k_ecrecover is the chunk roots the notary runs beside the tx kernel on its
-// side stream (~1 ms of every 8.5 ms step shares the SIMDs), not the decode.
+// noise.  r06: the sighash preimage and R / S (~200 of a tx's byte reads) are gathered as dwords
+// (BlobView::dword: two aligned loads per four bytes, issued together), which also freed registers
+// (256 -> 247 VGPRs, scratch 784 -> 448 B per lane): tx kernels -1.8 to -2.0 %, 8.80 ns per tx at 128
+// shards (profiles/r06/ab/notary_gather.txt).  The RLP headers stay byte reads (each depends on the last).
+GSV_DI uint32_t ld_g32(uintptr_t a) { return *(const __attribute__((address_space(1))) uint32_t*)a; }
+
 struct BlobView {
     const uint8_t* base;  // first chunk of the blob
+    uintptr_t hi;         // the last 4-byte-aligned dword holding a byte of the blob's chunks
     GSV_DI uint8_t at(uint32_t k) const { return base[(size_t)(k / 31) * 32 + 1 + k % 31]; }
+    // Data bytes k .. k+3 as one little-endian word (byte k lowest), read through the chunk map as two
+    // aligned dwords and realigned; when the chunk ends among them the next chunk's indicator byte is
+    // dropped.  Past the blob's data the bytes are unspecified (callers mask them); no dword past the
+    // blob's chunks is read, so every read holds a byte of the body.
+    GSV_DI uint32_t dword(uint32_t k) const {
+        uint32_t c = k / 31u, r = k - 31u * c;
+        uintptr_t a = (uintptr_t)base + 32u * (uintptr_t)c + 1u + r;
+        uint32_t sh = (uint32_t)a & 3u;
+        uintptr_t A = a & ~(uintptr_t)3;
+        uint32_t x0 = ld_g32(A <= hi ? A : hi), x1 = ld_g32(A + 4 <= hi ? A + 4 : hi);
+        uint32_t v = __builtin_amdgcn_alignbyte(x1, x0, sh);  // bytes a .. a+3
+        // r > 27: 31 - r (1..3) data bytes, the indicator, then the next chunk's data
+        uint32_t b4 = (x1 >> (8u * sh)) & 0xFFu;              // byte a+4
+        uint32_t m = r > 27u ? (1u << (8u * (31u - r))) - 1u : ~0u;
+        return (v & m) | (((v >> 8) | (b4 << 24)) & ~m);
+    }
 };
 
 struct RItem {
@@ -151,11 +172,19 @@ GSV_DI uint32_t bitlen_item(const BlobView& b, const RItem& it) {  // canonical:
     return 8 * (it.n - 1) + (32 - __builtin_clz((uint32_t)b.at(it.off)));
 }
 
+// 32-bit limb w of the big-endian unsigned integer item (it.n <= 32): its bytes n-4-4w .. n-1-4w
+GSV_DI uint32_t item_limb(const BlobView& b, const RItem& it, int w) {
+    int32_t e = (int32_t)it.n - 4 - 4 * w;  // item position of the limb's most significant byte
+    uint32_t d = b.dword(it.off + (uint32_t)(e > 0 ? e : 0));
+    d = e < 0 ? (e > -4 ? d << (8u * (uint32_t)(-e)) : 0u) : d;  // positions before the item read as zero
+    return __builtin_bswap32(d);
+}
+
 // Big-endian 64-byte helpers for V values longer than 8 bytes (rare; mirrors tx_host.hip be_sub)
 __device__ __noinline__ uint32_t v_big_path(const uint8_t* blob_base, uint32_t voff, uint32_t vn,
                                             const uint8_t* __restrict__ cid64, uint8_t* vv_low,
                                             uint32_t* vv_big) {
-    BlobView b{blob_base};
+    BlobView b{blob_base, 0};  // at() only
     if (vn > 64) return GSV_ST_INVALID_CHAIN_ID;  // be_sub rejects an > 64
     uint8_t V[64], t[64], chain[64];
     for (int i = 0; i < 64; i++) V[i] = 0;
@@ -200,40 +229,55 @@ __device__ __noinline__ uint32_t v_big_path(const uint8_t* blob_base, uint32_t v
 // The sighash preimage as a byte stream: [list header][blob bytes seg_lo .. seg_hi)[suffix]
 struct PreStream {
     BlobView b;
-    uint64_t hdr;       // header bytes, big-endian in the low hlen bytes
+    uint64_t hdr;       // header bytes, big-endian in the low hlen (<= 5) bytes
     uint32_t hlen;
     uint32_t seg_lo, seg_len;
-    const uint8_t* suffix;  // uniform (kernel argument buffer)
+    const uint8_t* suffix;  // uniform; zero bytes at [-8, 0) and [slen, slen + 8) (notary_shape layout)
     uint32_t slen;
     GSV_DI uint32_t total() const { return hlen + seg_len + slen; }
-    GSV_DI uint8_t at(uint32_t k) const {
-        if (k < hlen) return (uint8_t)(hdr >> (8 * (hlen - 1 - k)));
-        k -= hlen;
-        if (k < seg_len) return b.at(seg_lo + k);
-        return suffix[k - seg_len];
+    // stream bytes sp .. sp+3 (sp a multiple of 4) as one little-endian word, zero past the stream
+    GSV_DI uint32_t dword(uint32_t sp, uint64_t hle) const {
+        uint32_t out = sp < 8u ? (uint32_t)(hle >> (8u * sp)) : 0u;  // header (stream bytes < hlen <= 5)
+        int32_t e = (int32_t)sp - (int32_t)hlen;                       // segment position of byte 0
+        // every read is unconditional (clamped into the blob's chunks / the padded suffix buffer) and
+        // masked afterwards, so a block's loads issue back to back
+        uint32_t d = b.dword(seg_lo + (uint32_t)(e > 0 ? e : 0));
+        d = e < 0 ? (e > -4 ? d << (8u * (uint32_t)(-e)) : 0u) : d;  // the first -e bytes are header
+        int32_t vh = (int32_t)seg_len - e;                             // bytes before the segment's end
+        d = vh >= 4 ? d : vh > 0 ? d & ((1u << (8u * (uint32_t)vh)) - 1u) : 0u;
+        out |= d;
+        int32_t f = e - (int32_t)seg_len;  // suffix position of byte 0 (zero-padded buffer)
+        int32_t fc = f < -4 ? -4 : f > (int32_t)slen ? (int32_t)slen : f;
+        uintptr_t q = (uintptr_t)(suffix + fc);
+        uintptr_t Q = q & ~(uintptr_t)3;
+        uint32_t x = __builtin_amdgcn_alignbyte(ld_g32(Q + 4), ld_g32(Q), (uint32_t)q & 3u);
+        int32_t vs = (int32_t)slen - f;  // bytes before the stream's end (slen is 0 for unprotected txs,
+                                         // whose lanes still read the buffer's suffix)
+        out |= vs >= 4 ? x : vs > 0 ? x & ((1u << (8u * (uint32_t)vs)) - 1u) : 0u;
+        return out;
     }
 };
 
-// Keccak-256 over the stream (crypto/sha3/sha3.go:98-157: rate 136, dsbyte 0x01)
+// Keccak-256 over the stream (crypto/sha3/sha3.go:98-157: rate 136, dsbyte 0x01), each rate block
+// gathered as 34 little-endian dwords: the blob bytes through BlobView::dword (two aligned loads per four
+// bytes, all of a block's loads independent), the header from a register, the suffix from its
+// zero-padded buffer.  r05 read the stream a byte at a time (136 dependent byte loads and ~6,300
+// instructions per block); a timing run with the preimage reads removed bounded what the stream's reads
+// cost at 1.6-2.2 % of k_notary_tx (profiles/r06/ab/notary_fake_sighash.txt).
 GSV_DI void keccak_stream(uint64_t a[25], const PreStream& s) {
 #pragma unroll
     for (int k = 0; k < 25; k++) a[k] = 0;
+    // header bytes in stream order: byte j of hle = stream byte j (j < hlen)
+    const uint64_t hle = __builtin_bswap64(s.hdr) >> (8u * (8u - s.hlen));
     uint32_t len = s.total(), pos = 0;
     while (true) {
         uint32_t rem = len - pos;  // bytes left; the final block when rem < 136
         bool final = rem < 136;
 #pragma unroll
         for (int w = 0; w < 17; w++) {
-            uint64_t v = 0;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                uint32_t q = (uint32_t)(w * 8 + j);
-                uint64_t byte = 0;
-                if (q < rem) byte = s.at(pos + q);
-                if (final && q == rem) byte ^= 0x01;
-                if (final && q == 135) byte ^= 0x80;
-                v |= byte << (8 * j);
-            }
+            uint64_t v = (uint64_t)s.dword(pos + 8u * w, hle) | ((uint64_t)s.dword(pos + 8u * w + 4u, hle) << 32);
+            if (final && (rem >> 3) == (uint32_t)w) v ^= 0x01ull << (8u * (rem & 7u));
+            if (final && w == 16) v ^= 0x8000000000000000ULL;
             a[w] ^= v;
         }
         keccakf(a);
@@ -263,7 +307,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
     uint32_t vbyte = 0, vbig = 1, homestead = 1;
     if (active) {
         BlobRec br = blobs[(size_t)shard * max_txs + t];
-        BlobView b{bodies + body_off[shard] + (size_t)br.first_chunk * 32};
+        const uint8_t* bb = bodies + body_off[shard] + (size_t)br.first_chunk * 32;
+        BlobView b{bb, ((uintptr_t)bb + 32u * (uintptr_t)br.nchunks - 1u) & ~(uintptr_t)3};
         RItem outer, f[9];
         uint32_t used = rlp_item(b, 0, br.len, outer);
         bool ok = used && used == br.len && outer.list;
@@ -351,20 +396,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSV_ECR_WAV
             // R, S (recoverPlain, :222-234): > 32 bytes cannot pass ValidateSignatureValues
             if (f[7].n > 32 || f[8].n > 32) vbig = 1;
             else {
+                // limb w (little-endian 32-bit) = item bytes n-4-4w .. n-1-4w, byte-reversed; bytes before
+                // the item's start are zero
 #pragma unroll
                 for (int w = 0; w < 8; w++) {
-                    uint32_t rv = 0, sv = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        int pos = 31 - (4 * w + j);  // big-endian byte index of bit group (w, j)
-                        int ri = pos - (32 - (int)f[7].n), si = pos - (32 - (int)f[8].n);
-                        uint32_t rbyte = (ri >= 0) ? b.at(f[7].off + (uint32_t)ri) : 0u;
-                        uint32_t sbyte = (si >= 0) ? b.at(f[8].off + (uint32_t)si) : 0u;
-                        rv |= rbyte << (8 * j);
-                        sv |= sbyte << (8 * j);
-                    }
-                    r[w] = rv;
-                    s[w] = sv;
+                    r[w] = item_limb(b, f[7], w);
+                    s[w] = item_limb(b, f[8], w);
                 }
             }
         }

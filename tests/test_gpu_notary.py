@@ -143,3 +143,50 @@ def test_tx_sender_batch_golden(ctx, oracle):
     for i, v in enumerate(vec["homestead"]):
         s, a = oracle.tx_sender(home[i], 1, 1)
         assert st[i] == s and (s != 0 or bytes(addr[i]) == a)
+
+
+def _signed_tx(oracle, key, nonce, data, chain_id, eip155=True, want_zero=None):
+    """An EIP-155 (or unprotected Homestead) transaction signed with `key`; want_zero = "r" / "s" retries
+    the signing nonce until that value's top byte is zero (a 31-byte or shorter RLP string)."""
+    to = bytes(range(1, 21))
+    fields = (oracle.rlp_uint(nonce) + oracle.rlp_uint(20 * 10 ** 9) + oracle.rlp_uint(21000 + len(data)) +
+              oracle.rlp_string(to) + oracle.rlp_uint(10 ** 18 + nonce) + oracle.rlp_string(data))
+    pre = fields + (oracle.rlp_uint(chain_id) + b"\x80\x80" if eip155 else b"")
+    h = oracle.keccak256(oracle.rlp_list(pre))
+    for k in range(1, 5000):
+        sig = oracle.secp_sign(h, key, k.to_bytes(32, "big"))
+        if want_zero is None or sig[0 if want_zero == "r" else 32] == 0:
+            break
+    else:
+        raise AssertionError("no signature with the wanted leading zero")
+    v = sig[64] + (35 + 2 * chain_id if eip155 else 27)
+    r, s = int.from_bytes(sig[:32], "big"), int.from_bytes(sig[32:64], "big")
+    return oracle.rlp_list(fields + oracle.rlp_uint(v) + oracle.rlp_uint(r) + oracle.rlp_uint(s))
+
+
+@pytest.mark.parametrize("chain_id", [1, 137, 2 ** 31 + 11, 2 ** 63 + 5, 2 ** 100 + 7])
+def test_notary_preimage_shapes(ctx, oracle, chain_id):
+    """The sighash preimage and R / S are gathered as little-endian dwords through the chunk map
+    (notary.hip BlobView::dword, PreStream::dword, item_limb): data fields of 0-1,100 bytes (list
+    headers of one to three bytes, preimages of one to nine rate blocks, every chunk phase), chain ids
+    whose rlp suffix is 3 to 16 bytes (V above 64 bits takes v_big_path), unprotected transactions in
+    the same body, and R or S with a zero top byte (31-byte strings).  Statuses and senders against the
+    oracle's types.Sender, and every sender against the signing key's address."""
+    key = bytes.fromhex("4c0883a69102937d6231471b5dbb6204fe5129617082792ae468d01a3f362318")
+    pub = oracle.secp_pubkey(key)
+    addr = oracle.keccak256(pub[1:])[12:]
+    rng = random.Random(chain_id % 1000)
+    txs = []
+    for i, n in enumerate([0, 1, 54, 55, 56, 57, 120, 135, 136, 137, 250, 400, 1100]):
+        txs.append(_signed_tx(oracle, key, i, bytes(rng.getrandbits(8) for _ in range(n)), chain_id))
+    txs.append(_signed_tx(oracle, key, 50, b"\x01\x02", chain_id, eip155=False))
+    txs.append(_signed_tx(oracle, key, 51, bytes(200), chain_id, eip155=False))
+    txs.append(_signed_tx(oracle, key, 52, b"", chain_id, want_zero="r"))
+    txs.append(_signed_tx(oracle, key, 53, bytes(77), chain_id, want_zero="s"))
+    for pad in range(1, 4):  # shift every later transaction's chunk phase
+        txs.append(_signed_tx(oracle, key, 60 + pad, bytes(pad * 9), chain_id))
+    body = oracle.blob_serialize(txs)
+    _, ntx, _, senders, status = _check(ctx, oracle, [body], chain_id, 0, 64)
+    assert ntx[0] == len(txs)
+    assert (status[0, :len(txs)] == ST_OK).all(), status[0, :len(txs)]
+    assert all(bytes(senders[0, t]) == addr for t in range(len(txs)))
