@@ -29,7 +29,14 @@ struct BlobRec {
 
 // ---------------------------------------------------------------- blob index (marshal.go:144-198)
 constexpr int BI_THREADS = 1024;
+constexpr uint32_t BI_MAX_CHUNKS = (1u << 20) / 32;  // bodies are <= 2^20 bytes (notary_shape refuses more)
+constexpr int BI_BATCH = 8;                          // indicator loads in flight per thread
 
+// The indicator bytes (byte 0 of every chunk) are first copied to LDS by coalesced loads — thread t reads
+// chunks t, t + 1,024, ..., eight loads in flight — and both passes over a thread's contiguous run of
+// chunks read them from there.  r05 read them in those passes straight from HBM, one dependent byte load
+// per chunk (two runs of 32 per thread at 1 MiB): 84.6 -> 40.8 us per 100-shard step, notary leg +0.5 %
+// (profiles/r06/ab/blob_index_lds.txt).
 __global__ __launch_bounds__(BI_THREADS) void k_blob_index(const uint8_t* __restrict__ bodies,
                                                           const uint64_t* __restrict__ body_off,
                                                           const uint32_t* __restrict__ body_len,
@@ -37,15 +44,31 @@ __global__ __launch_bounds__(BI_THREADS) void k_blob_index(const uint8_t* __rest
                                                           uint32_t* __restrict__ ntx) {
     __shared__ uint32_t s_cnt[BI_THREADS];
     __shared__ int32_t s_last[BI_THREADS];
+    __shared__ uint8_t s_ind[BI_MAX_CHUNKS];
     const uint32_t shard = blockIdx.x, t = threadIdx.x;
     const uint8_t* body = bodies + body_off[shard];
-    const uint32_t chunks = body_len[shard] / 32;  // a trailing partial chunk is ignored (marshal.go:145)
+    // a trailing partial chunk is ignored (marshal.go:145)
+    const uint32_t chunks = min(body_len[shard] / 32, BI_MAX_CHUNKS);
+    for (uint32_t b = t; b < chunks; b += BI_BATCH * BI_THREADS) {
+        uint8_t v[BI_BATCH];
+#pragma unroll
+        for (int k = 0; k < BI_BATCH; k++) {
+            uint32_t c = b + k * BI_THREADS;
+            v[k] = c < chunks ? body[(size_t)c * 32] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < BI_BATCH; k++) {
+            uint32_t c = b + k * BI_THREADS;
+            if (c < chunks) s_ind[c] = v[k];
+        }
+    }
+    __syncthreads();
     const uint32_t per = (chunks + BI_THREADS - 1) / BI_THREADS;
     const uint32_t c0 = t * per, c1 = min(chunks, c0 + per);
     uint32_t cnt = 0;
     int32_t last = -1;
     for (uint32_t c = c0; c < c1; c++)
-        if (body[(size_t)c * 32] & 0x1F) {
+        if (s_ind[c] & 0x1F) {
             cnt++;
             last = (int32_t)c;
         }
@@ -64,7 +87,7 @@ __global__ __launch_bounds__(BI_THREADS) void k_blob_index(const uint8_t* __rest
     uint32_t base = s_cnt[t] - cnt;
     int32_t prev = t ? s_last[t - 1] : -1;
     for (uint32_t c = c0; c < c1; c++) {
-        uint8_t ind = body[(size_t)c * 32];
+        uint8_t ind = s_ind[c];
         uint32_t tl = ind & 0x1F;
         if (!tl) continue;
         if (base < max_txs) {
