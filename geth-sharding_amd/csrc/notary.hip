@@ -111,7 +111,9 @@ __global__ __launch_bounds__(BI_THREADS) void k_blob_index(const uint8_t* __rest
 // noise.  r06: the sighash preimage and R / S (~200 of a tx's byte reads) are gathered as dwords
 // (BlobView::dword: two aligned loads per four bytes, issued together), which also freed registers
 // (256 -> 247 VGPRs, scratch 784 -> 448 B per lane): tx kernels -1.8 to -2.0 %, 8.80 ns per tx at 128
-// shards (profiles/r06/ab/notary_gather.txt).  The RLP headers stay byte reads (each depends on the last).
+// shards (profiles/r06/ab/notary_gather.txt).  The RLP headers stay byte reads (each depends on the last);
+// reading the integer items' lead bytes together and V as two dwords measured within noise (r06,
+// profiles/r06/ab/notary_lead_bytes.txt).
 GSV_DI uint32_t ld_g32(uintptr_t a) { return *(const __attribute__((address_space(1))) uint32_t*)a; }
 
 struct BlobView {
