@@ -1156,13 +1156,71 @@ hipError_t launch_derive_sha_plan(const TriePlan* plan, uint32_t nlists, const u
 
 // ================================================================ Proof of Custody body expansion
 // sharding/collation.go:124-136: salted[k*(s+1) .. +s) = salt, salted[k*(s+1)+s] = body[k]; an empty
-// body gives salted = salt.  One thread per 4 output bytes, grid.y = body; in_off holds (start, end)
-// pairs per body, out_off the 16-byte aligned output starts.
+// body gives salted = salt.  grid.y = body; in_off holds (start, end) pairs per body, out_off the
+// 16-byte aligned output starts.
+//
+// One thread per 16 output bytes, one dwordx4 store: the salted stream is the period-(s+1) pattern
+// salt || 0 with body byte k in slot k*(s+1)+s.  Each workgroup stages the pattern (s + 1 + 24 bytes)
+// in LDS; a thread reads its 16 bytes at phase r0 as five aligned LDS dwords (fewer than 64 dwords
+// apart, so the lanes' different phases hit different banks) realigned with v_alignbyte, then ORs in
+// the <= ceil(16 / (s+1)) body bytes of its window.  r05 wrote one dword per thread from per-byte
+// salt and body loads: 1,583 -> 606 us per 100 x 1 MiB batch at a 20-byte salt (3.5 TB/s of writes), the
+// POC leg 5,048-5,080 -> 5,309 bodies/s (r06, profiles/r06/ab/poc_expand.txt).
+constexpr uint32_t POC_SALT_LDS = 8192;  // longer salts take k_poc_expand_bytes
+
 __global__ __launch_bounds__(256) void k_poc_expand(const uint8_t* __restrict__ bodies,
                                                     const uint64_t* __restrict__ in_off,
                                                     const uint64_t* __restrict__ out_off,
                                                     const uint8_t* __restrict__ salt, uint32_t slen,
                                                     uint8_t* out) {
+    __shared__ uint32_t s_pat[(POC_SALT_LDS + 1 + 24 + 3) / 4 + 1];
+    const uint32_t per = slen + 1;
+    uint8_t* pat8 = (uint8_t*)s_pat;
+    for (uint32_t k = threadIdx.x; k < per + 24; k += 256) {
+        uint32_t m = k % per;
+        pat8[k] = m < slen ? salt[m] : 0;
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.y;
+    const uint64_t n_in = in_off[2 * b + 1] - in_off[2 * b];
+    const uint64_t n_out = n_in ? n_in * per : slen;
+    const uint64_t k0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (k0 >= n_out) return;
+    const uint8_t* src = bodies + in_off[2 * b];
+    uint8_t* dst = out + out_off[b];
+    const uint64_t q0 = k0 / per;
+    const uint32_t r0 = (uint32_t)(k0 - q0 * per);
+    const uint32_t a = r0 >> 2, sh = r0 & 3u;
+    uint32_t d[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) d[j] = s_pat[a + j];
+    uint32_t w0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh), w1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+    uint32_t w2 = __builtin_amdgcn_alignbyte(d[3], d[2], sh), w3 = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+    if (n_in) {
+        uint64_t q = q0;
+        for (uint32_t u = slen - r0; u < 16u && q < n_in; u += per, q++) {  // the window's body bytes
+            uint32_t v = (uint32_t)src[q] << (8u * (u & 3u));
+            uint32_t i = u >> 2;
+            w0 |= i == 0 ? v : 0u;
+            w1 |= i == 1 ? v : 0u;
+            w2 |= i == 2 ? v : 0u;
+            w3 |= i == 3 ? v : 0u;
+        }
+    }
+    if (k0 + 16 <= n_out) {
+        *(uint4*)(dst + k0) = make_uint4(w0, w1, w2, w3);
+    } else {
+        uint32_t w[4] = {w0, w1, w2, w3};
+        for (uint32_t u = 0; k0 + u < n_out; u++) dst[k0 + u] = (uint8_t)(w[u >> 2] >> (8u * (u & 3u)));
+    }
+}
+
+// salts longer than POC_SALT_LDS: one thread per 4 output bytes, salt and body bytes read from HBM
+__global__ __launch_bounds__(256) void k_poc_expand_bytes(const uint8_t* __restrict__ bodies,
+                                                          const uint64_t* __restrict__ in_off,
+                                                          const uint64_t* __restrict__ out_off,
+                                                          const uint8_t* __restrict__ salt, uint32_t slen,
+                                                          uint8_t* out) {
     uint32_t b = blockIdx.y;
     uint64_t n_in = in_off[2 * b + 1] - in_off[2 * b];
     uint64_t n_out = n_in ? n_in * (slen + 1) : slen;
@@ -1172,20 +1230,13 @@ __global__ __launch_bounds__(256) void k_poc_expand(const uint8_t* __restrict__ 
     uint8_t* dst = out + out_off[b];
     uint64_t q = k0 / (slen + 1);
     uint32_t r = (uint32_t)(k0 - q * (slen + 1));
-    uint8_t o[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-        o[u] = k0 + u >= n_out ? 0 : (!n_in || r < slen) ? salt[r] : src[q];
+        if (k0 + u < n_out) dst[k0 + u] = (!n_in || r < slen) ? salt[r] : src[q];
         if (++r > slen) {
             r = 0;
             q++;
         }
-    }
-    if (k0 + 4 <= n_out) {
-        *(uint32_t*)(dst + k0) = (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) |
-                                 ((uint32_t)o[3] << 24);
-    } else {
-        for (uint64_t u = 0; k0 + u < n_out; u++) dst[k0 + u] = o[u];
     }
 }
 
@@ -1193,9 +1244,15 @@ hipError_t launch_poc_expand(const uint8_t* d_bodies, const uint64_t* d_in_off, 
                              uint32_t nbodies, uint64_t max_out, const uint8_t* d_salt, uint32_t slen, uint8_t* d_out,
                              hipStream_t st) {
     if (!nbodies || !max_out) return hipSuccess;
-    uint64_t blocks = (max_out + 1023) / 1024;
-    hipLaunchKernelGGL(k_poc_expand, dim3((unsigned)blocks, nbodies), dim3(256), 0, st, d_bodies, d_in_off,
-                       d_out_off, d_salt, slen, d_out);
+    if (slen <= POC_SALT_LDS) {
+        uint64_t blocks = (max_out + 4095) / 4096;
+        hipLaunchKernelGGL(k_poc_expand, dim3((unsigned)blocks, nbodies), dim3(256), 0, st, d_bodies, d_in_off,
+                           d_out_off, d_salt, slen, d_out);
+    } else {
+        uint64_t blocks = (max_out + 1023) / 1024;
+        hipLaunchKernelGGL(k_poc_expand_bytes, dim3((unsigned)blocks, nbodies), dim3(256), 0, st, d_bodies,
+                           d_in_off, d_out_off, d_salt, slen, d_out);
+    }
     return hipGetLastError();
 }
 

@@ -85,6 +85,21 @@ def test_poc_batch_vs_oracle(ctx, oracle):
         assert bytes(out[i]) == oracle.calculate_poc(b, salt), i
 
 
+@pytest.mark.parametrize("slen", [0, 1, 3, 15, 16, 17, 20, 33, 255, 9000])
+def test_poc_salt_lengths_vs_oracle(ctx, oracle, slen):
+    """k_poc_expand writes 16 salted bytes per thread from the period-(s+1) pattern staged in LDS plus
+    the window's body bytes (one or more per window below s = 15, at most one from s = 15 up; every
+    window phase); salts past its LDS bound (8,192 bytes) take k_poc_expand_bytes.  Bodies of 0-1,037
+    bytes, so salted lengths end at every phase of a 16-byte store."""
+    rng = np.random.default_rng(100 + slen)
+    salt = rng.integers(0, 256, slen, dtype=np.uint8).tobytes()
+    lens = [0, 1, 2, 15, 16, 17, 100, 1037] if slen < 9000 else [0, 1, 7, 100]
+    bodies = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    out = ctx.collation_poc_batch(bodies, salt)
+    for i, b in enumerate(bodies):
+        assert bytes(out[i]) == oracle.calculate_poc(b, salt), (slen, len(b))
+
+
 def test_poc_size_limit(ctx):
     import gsv
     with pytest.raises(gsv.GsvError):
