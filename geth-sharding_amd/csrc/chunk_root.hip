@@ -1013,7 +1013,14 @@ GSV_DI uint64_t low_bytes(int32_t n) { return n <= 0 ? 0ull : n >= 8 ? ~0ull : (
 // Keccak-256 of header(H bytes in hw0/hw1) || v[0..L) without materialising the message: each rate
 // block is read from v as <= 35 aligned dwords (only those holding a value byte) realigned with
 // v_alignbyte, bytes outside the value masked, the header OR-ed into block 0's first two words.
-GSV_DI void keccak_hdr_value(uint32_t h[8], uint64_t hw0, uint64_t hw1, uint32_t H, const uint8_t* v, uint32_t L) {
+typedef uint32_t u32x4a4_cr __attribute__((ext_vector_type(4), aligned(4)));
+// whole (wave-uniform): each 16-byte group that holds a value byte is read as one dwordx4 — the up to 15
+// bytes it reads outside the value belong to the batch's other values (the caller checks >= 32 bytes
+// of the batch on both sides) and are masked like the per-dword path's (r06, as k_keccak256's final
+// block: load_block_tail; k_derive_leaf 126.6 -> 118.7 us per tx-root step, the leg +3-5 %,
+// profiles/r06/ab/derive_leaf.txt)
+GSV_DI void keccak_hdr_value(uint32_t h[8], uint64_t hw0, uint64_t hw1, uint32_t H, const uint8_t* v, uint32_t L,
+                             bool whole) {
     uint64_t a[25];
 #pragma unroll
     for (int k = 0; k < 25; k++) a[k] = 0;
@@ -1024,11 +1031,24 @@ GSV_DI void keccak_hdr_value(uint32_t h[8], uint64_t hw0, uint64_t hw1, uint32_t
         uintptr_t sa = (uintptr_t)v - H + (uintptr_t)base;  // source of block byte 0 (value coordinates)
         const uint32_t* q = (const uint32_t*)(sa & ~(uintptr_t)3);
         uint32_t sh = (uint32_t)(sa & 3u);
-        uint32_t d[35];
+        uint32_t d[36];
+        if (whole) {
 #pragma unroll
-        for (int j = 0; j < 35; j++) {
-            int32_t b0 = 4 * j - (int32_t)sh;  // block position of dword j's first byte
-            d[j] = (b0 + 4 > vlo && b0 < vhi) ? q[j] : 0u;
+            for (int g = 0; g < 9; g++) {
+                int32_t b0 = 16 * g - (int32_t)sh;  // block position of the group's first byte
+                u32x4a4_cr x = {0u, 0u, 0u, 0u};
+                if (b0 + 16 > vlo && b0 < vhi) x = *(const u32x4a4_cr*)(q + 4 * g);
+                d[4 * g] = x.x;
+                d[4 * g + 1] = x.y;
+                d[4 * g + 2] = x.z;
+                d[4 * g + 3] = x.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 36; j++) {
+                int32_t b0 = 4 * j - (int32_t)sh;  // block position of dword j's first byte
+                d[j] = (j < 35 && b0 + 4 > vlo && b0 < vhi) ? q[j] : 0u;
+            }
         }
         int32_t rem = (int32_t)len - base;  // in the final block: position of the 0x01 pad byte
 #pragma unroll
@@ -1057,7 +1077,7 @@ GSV_DI void keccak_hdr_value(uint32_t h[8], uint64_t hw0, uint64_t hw1, uint32_t
 // encoded [compact, string(value)] (trie/hasher.go:113-145 via node.go EncodeRLP); inlined into its
 // parent when the RLP is < 32 bytes, else hashed; a list of one item is that leaf, hashed as root.
 __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__ vals,
-                                                     const uint64_t* __restrict__ voff,
+                                                     const uint64_t* __restrict__ voff, uint64_t vend,
                                                      uint8_t* lmsg,
                                                      const uint64_t* __restrict__ leaf_base,
                                                      const uint16_t* __restrict__ leaf_depth, uint32_t N,
@@ -1092,7 +1112,9 @@ __global__ __launch_bounds__(256) void k_derive_leaf(const uint8_t* __restrict__
         put_prefix(r, 0x80, L);
         if (r.n <= 16 && (N == 1 || r.n + L >= 32)) {
             uint32_t h[8];
-            keccak_hdr_value(h, r.w0, r.w1, r.n, v, L);
+            // whole 16-byte groups when every lane's value has >= 32 bytes of the batch on both sides
+            bool edge = voff[item] < voff[0] + 32 || voff[item + 1] + 32 > vend;
+            keccak_hdr_value(h, r.w0, r.w1, r.n, v, L, __builtin_amdgcn_ballot_w64(edge) == 0);
             if (N == 1) store_hash32(roots + (size_t)b * 32, h);
             else store_hashref_slot(s, h);
             return;
@@ -1127,14 +1149,14 @@ size_t derive_sha_scratch_bytes(const TriePlan* plan, uint32_t nlists) {
 }
 
 hipError_t launch_derive_sha_plan(const TriePlan* plan, uint32_t nlists, const uint8_t* d_vals,
-                                  const uint64_t* d_voff, const uint64_t* d_leaf_base, uint8_t* d_lmsg, uint8_t* d_leafrefs, uint8_t* d_scratch, uint8_t* d_roots,
+                                  const uint64_t* d_voff, uint64_t vend, const uint64_t* d_leaf_base, uint8_t* d_lmsg, uint8_t* d_leafrefs, uint8_t* d_scratch, uint8_t* d_roots,
                                   hipStream_t st, void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
                                   void* tctx) {
     const TriePlanHost& p = plan->h;
     if (nlists == 0 || p.N == 0 || !p.generic) return hipSuccess;
     uint64_t total = (uint64_t)p.N * nlists;
     if (timer_begin) timer_begin(tctx, GSV_K_DERIVE_LEAF);
-    hipLaunchKernelGGL(k_derive_leaf, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d_vals, d_voff,
+    hipLaunchKernelGGL(k_derive_leaf, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d_vals, d_voff, vend,
                        d_lmsg, d_leaf_base, plan->d_leaf_depth, p.N, nlists, d_leafrefs, d_roots);
     if (timer_end) timer_end(tctx, GSV_K_DERIVE_LEAF);
     hipError_t e = hipGetLastError();

@@ -107,6 +107,7 @@ struct Shape {
     std::vector<TrieGroup> dgroups;
     std::vector<uint32_t> dempty;
     size_t o_voff = 0, o_lmsg = 0, o_leafrefs = 0, o_dempty = 0;
+    uint64_t vend = 0;  // end of the batch's value bytes (absolute offset into the caller's vals)
     // SK_POC
     size_t o_io = 0, o_oo = 0, o_salt = 0, o_out = 0;
     uint64_t poc_max = 0;
@@ -1257,6 +1258,7 @@ int derive_shape(gsv_ctx* c, Shape& s, const uint64_t* voff, const uint64_t* lis
     s.o_leafrefs = L.add(total * 48);
     s.o_dempty = L.add(32);
     s.stage(s.o_voff, voff + list_off[0], total + 1);
+    s.vend = voff[list_off[n]];
     s.stage(s.o_dempty, EMPTY_ROOT, 32);
     for (auto& g : groups) {
         if (g.first == 0) {  // empty list -> emptyRoot (trie/trie.go:472-474)
@@ -1281,7 +1283,7 @@ int derive_shape(gsv_ctx* c, Shape& s, const uint64_t* voff, const uint64_t* lis
 int derive_run(gsv_ctx* c, const Shape& s, const uint8_t* d_vals, uint8_t* d_roots, hipStream_t st) {
     for (const TrieGroup& g : s.dgroups) {
         uint8_t* d_gr = s.at<uint8_t>(g.o_roots);
-        HIPCHK(gsv::launch_derive_sha_plan(g.plan.get(), g.count, d_vals, s.at<uint64_t>(s.o_voff),
+        HIPCHK(gsv::launch_derive_sha_plan(g.plan.get(), g.count, d_vals, s.at<uint64_t>(s.o_voff), s.vend,
                                            s.at<uint64_t>(g.o_base), s.at<uint8_t>(s.o_lmsg),
                                            s.at<uint8_t>(s.o_leafrefs), s.at<uint8_t>(g.o_scr), d_gr, st, hook_begin,
                                            hook_end, c));

@@ -39,7 +39,7 @@ hipError_t launch_chunk_root_plan(const TriePlan* plan, const uint8_t* d_bodies,
 // generic DeriveSha (any DerivableList) and the Proof-of-Custody salted body
 size_t derive_sha_scratch_bytes(const TriePlan* plan, uint32_t nlists);
 hipError_t launch_derive_sha_plan(const TriePlan* plan, uint32_t nlists, const uint8_t* d_vals,
-                                  const uint64_t* d_voff, const uint64_t* d_leaf_base, uint8_t* d_lmsg, uint8_t* d_leafrefs, uint8_t* d_scratch, uint8_t* d_roots,
+                                  const uint64_t* d_voff, uint64_t vend, const uint64_t* d_leaf_base, uint8_t* d_lmsg, uint8_t* d_leafrefs, uint8_t* d_scratch, uint8_t* d_roots,
                                   hipStream_t st, void (*timer_begin)(void*, int), void (*timer_end)(void*, int),
                                   void* tctx);
 hipError_t launch_poc_expand(const uint8_t* d_bodies, const uint64_t* d_in_off, const uint64_t* d_out_off,

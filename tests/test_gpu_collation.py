@@ -208,3 +208,30 @@ def test_dev_calls_on_two_streams_share_the_workspace_safely(ctx, oracle):
     p = pocs.cpu().numpy()
     for i, b in enumerate(pb):
         assert bytes(p[i]) == oracle.calculate_poc(b, salt), i
+
+
+def test_derive_sha_dev_tx_lists_at_batch_edges(ctx, oracle):
+    """k_derive_leaf reads a hashed leaf's value as whole 16-byte groups when every lane's value has
+    >= 32 bytes of the batch on both sides, and dword by dword in the waves at the batch's edges.  Here
+    the batch is a slice of the items (list_off starting past item 0, so bytes before it are other
+    items') of 100-160-byte values (the tx-root leg's shape) plus short and empty values, in a vals
+    buffer that ends at the last value with 0xff bytes after it."""
+    import torch
+    rng = np.random.default_rng(17)
+    sizes = [5, 200, 64, 3, 200, 1]
+    lists = [[rng.integers(0, 256, int(rng.choice([0, 1, 40, 100, 135, 150, 160])), dtype=np.uint8).tobytes()
+              for _ in range(n)] for n in sizes]
+    items = [x for lst in lists for x in lst]
+    voff = np.zeros(len(items) + 1, np.uint64)
+    voff[1:] = np.cumsum([len(x) for x in items])
+    list_off = np.cumsum([0] + sizes).astype(np.uint64)
+    flat = np.frombuffer(b"".join(items), np.uint8)
+    vals = torch.full((len(flat) + 64,), 0xff, dtype=torch.uint8, device="cuda")
+    vals[:len(flat)] = torch.from_numpy(flat.copy()).cuda()
+    sub = list_off[1:]  # the batch: lists 1.. (item 0's list is outside it)
+    roots = torch.zeros((len(sub) - 1, 32), dtype=torch.uint8, device="cuda")
+    ctx.derive_sha_batch_dev(vals, voff, sub, roots)
+    torch.cuda.synchronize()
+    r = roots.cpu().numpy()
+    for i, lst in enumerate(lists[1:]):
+        assert bytes(r[i]) == oracle.derive_sha(lst), (i, len(lst))
