@@ -688,6 +688,8 @@ GSV_DI void do_generic_lane(const PNode& nd, const PChild* __restrict__ children
 }
 
 // generic nodes of one height, over all bodies, above which one lane per node beats one wave per node
+// (r06: thresholds of 65,536 / 262,144 / never made the tx-root leg's 26 k-node first height 25 % slower,
+// profiles/r06/ab/gen_lane_mode.txt)
 constexpr uint64_t GEN_LANE_MODE_MIN = 4096;
 
 // Generic node (BRANCH / EXT / byte-mode root LEAF) handled by a 32-lane group: lane k writes
