@@ -164,12 +164,12 @@ def _signed_tx(oracle, key, nonce, data, chain_id, eip155=True, want_zero=None):
     return oracle.rlp_list(fields + oracle.rlp_uint(v) + oracle.rlp_uint(r) + oracle.rlp_uint(s))
 
 
-@pytest.mark.parametrize("chain_id", [1, 137, 2 ** 31 + 11, 2 ** 63 + 5, 2 ** 100 + 7])
+@pytest.mark.parametrize("chain_id", [0, 1, 137, 2 ** 31 + 11, 2 ** 63 + 5, 2 ** 100 + 7])
 def test_notary_preimage_shapes(ctx, oracle, chain_id):
     """The sighash preimage and R / S are gathered as little-endian dwords through the chunk map
     (notary.hip BlobView::dword, PreStream::dword, item_limb): data fields of 0-1,100 bytes (list
     headers of one to three bytes, preimages of one to nine rate blocks, every chunk phase), chain ids
-    whose rlp suffix is 3 to 16 bytes (V above 64 bits takes v_big_path), unprotected transactions in
+    whose rlp suffix is 3 to 16 bytes (chain id 0 included; V above 64 bits takes v_big_path), unprotected transactions in
     the same body, and R or S with a zero top byte (31-byte strings).  Statuses and senders against the
     oracle's types.Sender, and every sender against the signing key's address."""
     key = bytes.fromhex("4c0883a69102937d6231471b5dbb6204fe5129617082792ae468d01a3f362318")
