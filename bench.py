@@ -862,19 +862,43 @@ def leg_headers(ctx, stream, dev, ws, rank, args, sig):
     hst = torch.empty((nh,), dtype=torch.uint8, device=dev)
     hhash = torch.empty((nh, 32), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()  # the inputs were staged on torch's default stream
+    # consecutive batches in flight on dedicated-queue streams (--ecrecover-pipeline, as the recovery leg;
+    # the shape prepared at that depth, one instance per stream): one batch's header hashes and compare
+    # run beside the other batch's recovery
+    hdepth = max(1, args.ecrecover_pipeline)
+    ctx.set_pipeline_depth(hdepth)
     ctx.collation_header_verify_batch_dev(hsid, hroot, hper, hprop, sig, hst, None, hhash, None, stream=stream)
+    ctx.set_pipeline_depth(1)
     stream.synchronize()
     assert bool((hst == _lib.ST_PROPOSER_MISMATCH).all()), "header signatures failed to recover"
-    hsteps = 3
+    hstreams = pipeline_streams(ctx, hdepth, stream, dev)
+    houts = [(hst, hhash)] + [(torch.empty_like(hst), torch.empty_like(hhash)) for _ in range(hdepth - 1)]
+    for s_ in hstreams:
+        s_.wait_stream(stream)
+
+    def hstep(i):
+        st_, h_ = houts[i % hdepth]
+        ctx.collation_header_verify_batch_dev(hsid, hroot, hper, hprop, sig, st_, None, h_, None,
+                                              stream=hstreams[i % hdepth], prepare=False)
+
+    for i in range(hdepth):
+        hstep(i)
+    for s_ in hstreams:
+        s_.synchronize()
+    assert all(torch.equal(st_, hst) and torch.equal(h_, hhash) for st_, h_ in houts), \
+        "pipelined header results differ between instances"
+    hsteps = 3 * hdepth
     barrier(ws)
     t7 = time.perf_counter()
-    for _ in range(hsteps):
-        ctx.collation_header_verify_batch_dev(hsid, hroot, hper, hprop, sig, hst, None, hhash, None, stream=stream,
-                                              prepare=False)
-    stream.synchronize()
+    for i in range(hsteps):
+        hstep(i)
+    for s_ in hstreams:
+        s_.synchronize()
     barrier(ws)
     hdt = max_over_ranks(time.perf_counter() - t7, ws)
-    return {"headers_per_s": round(ws * nh * hsteps / hdt, 1), "headers": nh, "ms_per_step": round(hdt / hsteps * 1e3, 3)}
+    ctx.destroy_streams(hstreams)
+    return {"headers_per_s": round(ws * nh * hsteps / hdt, 1), "headers": nh, "ms_per_step": round(hdt / hsteps * 1e3, 3),
+            "batches_in_flight": hdepth}
 
 
 def pipeline_streams(ctx, depth, stream, dev):
