@@ -1112,10 +1112,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--legs", default=",".join(LEGS), help="comma list of " + ",".join(LEGS))
     ap.add_argument("--ecrecover-pipeline", type=int, default=2,
-                    help="streams consecutive ecrecover batches are spread over (2, the default since r06: two "
-                         "batches in flight on dedicated-queue streams, as the other legs; the roofline's "
-                         "kernel time then comes from a separate single-stream instrumented pass; 1: one "
-                         "stream, kernel time from HIP events over the timed region itself)")
+                    help="streams consecutive ecrecover (and collation-header) batches are spread over (2, the "
+                         "default since r06: two batches in flight on dedicated-queue streams, as the other legs; "
+                         "the roofline's kernel time then comes from a separate single-stream instrumented pass; "
+                         "1: one stream, kernel time from HIP events over the timed region itself)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="streams (shape instances) consecutive chunk-root batches are spread over")
     ap.add_argument("--pairing-pipeline", type=int, default=0,
