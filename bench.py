@@ -800,26 +800,39 @@ def leg_tx_root(ctx, stream, dev, ws, rank, args):
     nblk, ntx, lens, voff, vals_np = _tx_strings(rank)
     vals = torch.from_numpy(vals_np).to(dev)
     list_off = np.arange(nblk + 1, dtype=np.uint64) * ntx
-    troots = torch.empty((nblk, 32), dtype=torch.uint8, device=dev)
+    # consecutive batches on --pipeline streams with their own shape instances (as the chunk-root leg):
+    # one batch's latency-bound trie heights run beside the next batch's leaf hashing
+    tdepth = max(1, args.pipeline)
+    ctx.set_pipeline_depth(tdepth)
     ctx.derive_sha_prepare(voff, list_off)
+    ctx.set_pipeline_depth(1)
+    tstreams = pipeline_streams(ctx, tdepth, stream, dev)
+    trk = [torch.empty((nblk, 32), dtype=torch.uint8, device=dev) for _ in range(tdepth)]
+    troots = trk[0]
     torch.cuda.synchronize()  # the inputs were staged on torch's default stream
-    ctx.derive_sha_batch_dev(vals, voff, list_off, troots, stream=stream, prepare=False)
-    stream.synchronize()
+    for i in range(tdepth):
+        ctx.derive_sha_batch_dev(vals, voff, list_off, trk[i], stream=tstreams[i], prepare=False)
+    for s_ in tstreams:
+        s_.synchronize()
+    assert all(torch.equal(r, troots) for r in trk), "pipelined tx roots differ between instances"
     tsteps = 20  # (r04: 3 steps, a 1.3-ms timed region)
     barrier(ws)
     t5 = time.perf_counter()
-    for _ in range(tsteps):
-        ctx.derive_sha_batch_dev(vals, voff, list_off, troots, stream=stream, prepare=False)
-    stream.synchronize()
+    for i in range(tsteps):
+        ctx.derive_sha_batch_dev(vals, voff, list_off, trk[i % tdepth], stream=tstreams[i % tdepth], prepare=False)
+    for s_ in tstreams:
+        s_.synchronize()
     barrier(ws)
     tdt = max_over_ranks(time.perf_counter() - t5, ws)
+    ctx.destroy_streams(tstreams)
     if rank == 0 and not args.no_cpu_baseline:
         from oracle import oracle as O
         items = [vals_np[int(voff[j]):int(voff[j + 1])].tobytes() for j in range(ntx)]
         assert bytes(troots[0].cpu().numpy()) == O.derive_sha(items), "tx root mismatch vs oracle"
     return {"blocks_per_s": round(ws * nblk * tsteps / tdt, 1), "txs_per_s": round(ws * nblk * ntx * tsteps / tdt, 1),
             "MBps_of_tx_rlp": round(ws * float(voff[-1]) * tsteps / tdt / 1e6, 1),
-            "blocks": nblk, "txs_per_block": ntx, "ms_per_step": round(tdt / tsteps * 1e3, 3)}
+            "blocks": nblk, "txs_per_block": ntx, "ms_per_step": round(tdt / tsteps * 1e3, 3),
+            "pipeline_depth": tdepth}
 
 
 def leg_poc(ctx, stream, dev, ws, rank, args):
@@ -830,23 +843,35 @@ def leg_poc(ctx, stream, dev, ws, rank, args):
     pbodies = torch.from_numpy(prng.integers(0, 256, N_SHARDS * BODY, dtype=np.uint8)).to(dev)
     p_off = np.arange(N_SHARDS + 1, dtype=np.uint64) * BODY
     salt = bytes(range(1, 21))
-    pocs = torch.empty((N_SHARDS, 32), dtype=torch.uint8, device=dev)
+    # consecutive batches on --pipeline streams with their own shape instances (each holds its 2.1 GB of
+    # salted bodies): one batch's expansion and trie top run beside the other batch's leaf level
+    qdepth = max(1, args.pipeline)
+    ctx.set_pipeline_depth(qdepth)
     ctx.collation_poc_prepare(p_off, salt)
+    ctx.set_pipeline_depth(1)
+    qstreams = pipeline_streams(ctx, qdepth, stream, dev)
+    pk = [torch.empty((N_SHARDS, 32), dtype=torch.uint8, device=dev) for _ in range(qdepth)]
+    pocs = pk[0]
     torch.cuda.synchronize()  # the inputs were staged on torch's default stream
-    ctx.collation_poc_batch_dev(pbodies, p_off, salt, pocs, stream=stream, prepare=False)
-    stream.synchronize()
-    qsteps = 2
+    for i in range(qdepth):
+        ctx.collation_poc_batch_dev(pbodies, p_off, salt, pk[i], stream=qstreams[i], prepare=False)
+    for s_ in qstreams:
+        s_.synchronize()
+    assert all(torch.equal(r, pocs) for r in pk), "pipelined POC roots differ between instances"
+    qsteps = 2 * qdepth
     barrier(ws)
     t6 = time.perf_counter()
-    for _ in range(qsteps):
-        ctx.collation_poc_batch_dev(pbodies, p_off, salt, pocs, stream=stream, prepare=False)
-    stream.synchronize()
+    for i in range(qsteps):
+        ctx.collation_poc_batch_dev(pbodies, p_off, salt, pk[i % qdepth], stream=qstreams[i % qdepth], prepare=False)
+    for s_ in qstreams:
+        s_.synchronize()
     barrier(ws)
     qdt = max_over_ranks(time.perf_counter() - t6, ws)
+    ctx.destroy_streams(qstreams)
     return {"bodies_per_s": round(ws * N_SHARDS * qsteps / qdt, 2),
             "body_GBps": round(ws * N_SHARDS * BODY * qsteps / qdt / 1e9, 3),
             "salted_GBps": round(ws * N_SHARDS * BODY * 21 * qsteps / qdt / 1e9, 3),
-            "salt_bytes": 20, "ms_per_step": round(qdt / qsteps * 1e3, 3)}
+            "salt_bytes": 20, "ms_per_step": round(qdt / qsteps * 1e3, 3), "pipeline_depth": qdepth}
 
 
 def leg_headers(ctx, stream, dev, ws, rank, args, sig):
@@ -1117,7 +1142,8 @@ def main():
                          "the roofline's kernel time then comes from a separate single-stream instrumented pass; "
                          "1: one stream, kernel time from HIP events over the timed region itself)")
     ap.add_argument("--pipeline", type=int, default=2,
-                    help="streams (shape instances) consecutive chunk-root batches are spread over")
+                    help="streams (shape instances) consecutive chunk-root (and Keccak, tx-root, POC) batches "
+                         "are spread over")
     ap.add_argument("--pairing-pipeline", type=int, default=0,
                     help="streams (shape instances) consecutive pairing batches are spread over "
                          "(0 = auto: 6 below 65,536 checks per rank, else 1)")
