@@ -69,6 +69,25 @@ KECCAK_VALU_FLOOR_PER_PERM = 24 * 180
 # but this round could reach.
 KECCAK_ROUND_MIX = {"v_bitop3_b32": (120, 2.31), "v_xor_b32": (2, 2.37), "v_alignbit_b32": (58, 4.22)}
 KECCAK_MIX_CYCLES_PER_PERM = 24 * sum(n * c for n, c in KECCAK_ROUND_MIX.values())
+# A permutation whose output is only read as a Keccak-256 digest (the sponge's last) needs state words
+# 0..3 after the last round: its theta still needs all five column parities, but rho / pi / chi only the
+# diagonal that lands in row 0 — 38 v_bitop3 + 2 v_xor + 18 v_alignbit = 58 instructions instead of 180
+# (keccak_dev.cuh keccakf_split_digest, r06).  The floors and mix ceilings below price such a
+# permutation at 23 x 180 + 58 = 4,198, so doing less than the full permutation does not read as a
+# higher fraction.
+KECCAK_DIGEST_ROUND_MIX = {"v_bitop3_b32": 38, "v_xor_b32": 2, "v_alignbit_b32": 18}
+KECCAK_DIGEST_SAVING = 180 - sum(KECCAK_DIGEST_ROUND_MIX.values())             # 122 instructions
+KECCAK_DIGEST_MIX_SAVING = sum((n - KECCAK_DIGEST_ROUND_MIX[k]) * c for k, (n, c) in KECCAK_ROUND_MIX.items())
+
+
+def keccak_floor_per_perm(perms, digests):
+    """Mean VALU floor per permutation of a launch with `digests` of its `perms` permutations in digest form."""
+    return KECCAK_VALU_FLOOR_PER_PERM - KECCAK_DIGEST_SAVING * digests / perms
+
+
+def keccak_ceiling(perms, digests):
+    """Permutations/s at the instruction floor (VALU_ISSUE_PEAK wave64 instructions per SIMD-cycle)."""
+    return SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / keccak_floor_per_perm(perms, digests)
 # Peaks (tools/microbench_{int,lat,occ}.hip on MI355X: profiles/r01_microbench_int.txt,
 # profiles/r05/microbench_occ_ops.txt):
 #   VALU issue: CDNA4 SIMDs are 32 wide, a wave64 instruction issues over 2 cycles -> at most 0.5
@@ -123,14 +142,17 @@ def clock_fracs(units_per_launch, k, peak_units_per_s):
     return out
 
 
-def mix_ceiling(units_per_launch, ms):
+def mix_ceiling(units_per_launch, ms, digests=0):
     """The Keccak legs against the permutation's issue-cost ceiling (KECCAK_MIX_CYCLES_PER_PERM: the
-    compiled round's instructions at their measured SIMD cycles), beside the fixed instruction floor."""
-    peak = SIMDS * 64 * CLOCK / KECCAK_MIX_CYCLES_PER_PERM
-    out = {"mix_ceiling": round(peak / 1e9, 3), "mix_cycles_per_permutation": round(KECCAK_MIX_CYCLES_PER_PERM),
+    compiled round's instructions at their measured SIMD cycles; a digest permutation's last round at
+    KECCAK_DIGEST_ROUND_MIX), beside the fixed instruction floor."""
+    cyc = KECCAK_MIX_CYCLES_PER_PERM - KECCAK_DIGEST_MIX_SAVING * digests / units_per_launch
+    peak = SIMDS * 64 * CLOCK / cyc
+    out = {"mix_ceiling": round(peak / 1e9, 3), "mix_cycles_per_permutation": round(cyc),
            "mix_basis": "24 rounds x (" + " + ".join(f"{n} {k.replace('_b32', '')} x {c}" for k, (n, c) in
                                                      KECCAK_ROUND_MIX.items()) +
-                        ") SIMD-cycles, profiles/r05/microbench_occ_ops.txt"}
+                        ") SIMD-cycles, profiles/r05/microbench_occ_ops.txt; a digest permutation's last "
+                        "round " + " + ".join(f"{n} {k.replace('_b32', '')}" for k, n in KECCAK_DIGEST_ROUND_MIX.items())}
     if ms:
         out["frac_mix_ceiling"] = round(units_per_launch / (ms * 1e-3) / peak, 4)
     return out
@@ -500,18 +522,20 @@ def leg_chunk_root(ctx, stream, dev, ws, rank, args):
     bot_perms = N_SHARDS * BODY // 16
     k = pmc("void gsv::k_chunk_level<true>", "pmc_chunk_root.json")
     ipp = k["sq_insts_valu"] / bot_perms * 64 if k.get("sq_insts_valu") else None  # VALU instr per perm per lane
-    ceiling = SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / KECCAK_VALU_FLOOR_PER_PERM
+    floor = keccak_floor_per_perm(bot_perms, bot_perms)  # every bottom permutation is a digest
+    ceiling = keccak_ceiling(bot_perms, bot_perms)
     traffic = pmc_traffic(k)
     bot_ach = bot_perms / (bot_ms * 1e-3)
     roof = {"bound": "valu", "unit": "Gperm/s", "kernel": "k_chunk_level<BOTTOM>", "kernel_avg_ms": round(bot_ms, 4),
             "achieved": round(bot_ach / 1e9, 3), "peak": round(ceiling / 1e9, 3) if ceiling else None,
             "frac": round(bot_ach / ceiling, 4) if ceiling else None,
             "peak_basis": f"instruction floor: {VALU_ISSUE_PEAK} wave64 VALU instructions per SIMD-cycle x 1024 "
-                          f"SIMDs x 2.4 GHz x 64 lanes / {KECCAK_VALU_FLOOR_PER_PERM} VALU instructions per "
-                          "permutation (the fixed Keccak-f floor, bench.py KECCAK_VALU_FLOOR_PER_PERM)",
+                          f"SIMDs x 2.4 GHz x 64 lanes / {floor:.0f} VALU instructions per "
+                          "permutation (the fixed Keccak-f floor, 24 x 180, with the digest permutation's last "
+                          "round at 58: bench.py KECCAK_DIGEST_ROUND_MIX)",
             "valu_instr_per_permutation": round(ipp, 1) if ipp else None,
-            "valu_instr_over_floor": round(ipp / KECCAK_VALU_FLOOR_PER_PERM, 3) if ipp else None,
-            **clock_fracs(bot_perms, k, ceiling), **mix_ceiling(bot_perms, bot_ms),
+            "valu_instr_over_floor": round(ipp / floor, 3) if ipp else None,
+            **clock_fracs(bot_perms, k, ceiling), **mix_ceiling(bot_perms, bot_ms, bot_perms),
             "mean_waves_per_simd": k.get("mean_waves_per_simd"),
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
             # the body bytes read + every bottom node's raw 32-byte hash written into its parent's slot
@@ -657,11 +681,13 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
     # and address of every tx: one each for these <= 135-byte strings), both priced at their VALU peak
     # and summed as SIMD time; the permutations are converted to MAC-equivalents at the two peaks' ratio
     oc = opcount("notary_tx")
-    perm_peak = SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / KECCAK_VALU_FLOOR_PER_PERM
     roof = None
     if oc:
         ntx = nloc * NOTARY_TXS
         perms = nloc * PERMS_PER_MIB + 2 * ntx
+        # digest permutations counted: the bottom branch nodes (N / 16 per body); the chunk roots' other
+        # hashed nodes (< 4,400 per MiB) are priced at the full floor
+        perm_peak = keccak_ceiling(perms, nloc * BODY // 16)
         mac_eq = oc["mac_equiv"] * ntx + perms * PEAK_MAC / perm_peak
         kt = pmc("gsv::k_notary_tx", "pmc_notary.json")
         kb = pmc("gsv::k_blob_index", "pmc_notary.json")
@@ -673,7 +699,7 @@ def leg_notary(ctx, stream, dev, ws, rank, args):
                                   "mac_equiv_per_permutation": round(PEAK_MAC / perm_peak, 1),
                                   "mac_equiv": round(mac_eq)},
                 "basis": "v_mad_u64_u32 of k_notary_tx (profiles/{R}/opcount.json notary_tx) + Keccak-f "
-                         "permutations at the fixed instruction floor (KECCAK_VALU_FLOOR_PER_PERM), as SIMD "
+                         "permutations at the fixed instruction floor (bench.py keccak_floor_per_perm), as SIMD "
                          "time at the 2.4 GHz VALU peaks".format(R=ROUND),
                 "tx_kernels_frac": round(tx_work / (k_not * 1e-3) / PEAK_MAC, 4) if k_not else None,
                 "k_notary_tx": {"profiled_avg_ms": kt.get("avg_ms"),
@@ -768,17 +794,20 @@ def leg_keccak(ctx, stream, dev, ws, rank, args):
     perms = int(np.sum(lens // 136 + 1))
     k = pmc("gsv::k_keccak256", "pmc_keccak.json")
     ipp = k["sq_insts_valu"] / perms * 64 if k.get("sq_insts_valu") else None
-    ceiling = SIMDS * VALU_ISSUE_PEAK * CLOCK * 64 / KECCAK_VALU_FLOOR_PER_PERM
+    nmsg = nblk * ntx  # one digest permutation per message
+    floor = keccak_floor_per_perm(perms, nmsg)
+    ceiling = keccak_ceiling(perms, nmsg)
     ach = perms / (kavg * 1e-3)
     traffic = pmc_traffic(k)
     roof = {"bound": "valu", "unit": "Gperm/s", "kernel": "k_keccak256", "kernel_avg_ms": round(kavg, 4),
             "achieved": round(ach / 1e9, 3), "peak": round(ceiling / 1e9, 3) if ceiling else None,
             "frac": round(ach / ceiling, 4) if ceiling else None,
             "peak_basis": "instruction floor (as chunk_root.roofline: the fixed Keccak-f floor of "
-                          f"{KECCAK_VALU_FLOOR_PER_PERM} VALU instructions per permutation)",
+                          f"{KECCAK_VALU_FLOOR_PER_PERM} VALU instructions per permutation, a message's digest "
+                          f"permutation at {KECCAK_VALU_FLOOR_PER_PERM - KECCAK_DIGEST_SAVING}: {floor:.0f} on average)",
             "valu_instr_per_permutation": round(ipp, 1) if ipp else None,
-            "valu_instr_over_floor": round(ipp / KECCAK_VALU_FLOOR_PER_PERM, 3) if ipp else None,
-            **clock_fracs(perms, k, ceiling), **mix_ceiling(perms, kavg),
+            "valu_instr_over_floor": round(ipp / floor, 3) if ipp else None,
+            **clock_fracs(perms, k, ceiling), **mix_ceiling(perms, kavg, nmsg),
             "mean_waves_per_simd": k.get("mean_waves_per_simd"),
             "valu_issue_per_simd_cycle": k.get("valu_issue_per_simd_cycle"),
             "traffic": traffic, "algorithmic_bytes_per_launch": int(voff[-1]) + (nblk * ntx + 1) * 8 + nblk * ntx * 32,

@@ -328,7 +328,7 @@ GSV_DI void keccak_buf(uint32_t h[8], const uint8_t* p, uint32_t len) {
         if (k == 16) w ^= 0x8000000000000000ULL;
         a[k] ^= w;
     }
-    keccakf(a);
+    keccakf_digest(a);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         h[2 * k] = (uint32_t)a[k];
@@ -433,7 +433,7 @@ GSV_DI void do_bottom(const PNode& nd, const BodyBatch& bb, uint32_t body, uint8
 #pragma unroll
     for (int k = 11; k < 25; k++) a[k] = 0;
     a[16] ^= 0x8000000000000000ULL;
-    keccakf(a);
+    keccakf_digest(a);
     uint32_t h[8];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -522,7 +522,7 @@ GSV_DI void hash_hfull(uint32_t h[8], const uint32_t* __restrict__ H) {
     keccakf_split(al, ah);
     hf_load(w3, Hq);
     hf_absorb_block(al, ah, w3);
-    keccakf_split(al, ah);
+    keccakf_split_digest(al, ah);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         h[2 * k] = al[k];
@@ -1066,7 +1066,7 @@ GSV_DI void keccak_hdr_value(uint32_t h[8], uint64_t hw0, uint64_t hw1, uint32_t
             }
             a[k] ^= x;
         }
-        keccakf(a);
+        keccakf(a);  // keccakf_digest on the last block: 162 -> 186 registers in k_derive_leaf
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) {

@@ -110,7 +110,7 @@ GSV_DI void keccak_lds(uint8_t* out, const uint64_t* lds, uint32_t lane, uint32_
         if (k == 16) w ^= 0x8000000000000000ULL;
         a[k] ^= w;
     }
-    keccakf(a);
+    keccakf_digest(a);
 #pragma unroll
     for (int k = 0; k < 4; k++)
 #pragma unroll

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void k_keccak256(const uint8_t* __restrict__ d
         if (k == 16) x ^= 0x8000000000000000ULL;
         a[k] ^= x;
     }
-    keccakf(a);
+    keccakf_digest(a);
     store_hash(out32, i, a);
 }
 

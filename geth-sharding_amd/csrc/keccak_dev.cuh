@@ -66,9 +66,10 @@ GSV_DI void theta_rho_pi(uint32_t bl[25], uint32_t bh[25], const uint32_t al[25]
 // theta's column parities as 20 three-way v_bitop3, rot(C, 1) as 10 v_alignbit, theta's application as
 // 50 three-way v_bitop3, rho as 48 v_alignbit, chi as 50 v_bitop3, iota 2.  One round per loop
 // iteration (two measured equal, r05: profiles/r05/ab/chunk_levels5_unroll2.txt).
-GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) {
+template <int ROUNDS>
+GSV_DI void keccakf_rounds(uint32_t al[25], uint32_t ah[25]) {
 #pragma unroll 1
-    for (int round = 0; round < 24; round++) {
+    for (int round = 0; round < ROUNDS; round++) {
         uint32_t cl[5], ch[5], dl[5], dh[5];
 #pragma unroll
         for (int x = 0; x < 5; x++) {
@@ -97,6 +98,39 @@ GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) {
     }
 }
 
+GSV_DI void keccakf_split(uint32_t al[25], uint32_t ah[25]) { keccakf_rounds<24>(al, ah); }
+
+// The permutation whose output is only read as a Keccak-256 digest (state words 0..3, the sponge's
+// last squeeze): 23 full rounds, then the last round computes just those four words.  Row 0 after
+// pi is rho(theta(A)) of the diagonal x = y (B[k] = rot(A'[6k], r[6k])), and chi of words 0..3 reads
+// B[0..4]; theta still needs all five column parities.  20 + 10 + 10 + 8 + 8 + 2 = 58 instructions
+// instead of 180: 4,198 per digest permutation instead of 4,320 (-2.8 %).  Words 4..24 of the
+// state are left unspecified.
+GSV_DI void keccakf_split_digest(uint32_t al[25], uint32_t ah[25]) {
+    keccakf_rounds<23>(al, ah);
+    uint32_t cl[5], ch[5], dl[5], dh[5];
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+        cl[x] = kxor3(kxor3(al[x], al[x + 5], al[x + 10]), al[x + 15], al[x + 20]);
+        ch[x] = kxor3(kxor3(ah[x], ah[x + 5], ah[x + 10]), ah[x + 15], ah[x + 20]);
+    }
+#pragma unroll
+    for (int x = 0; x < 5; x++) krot<1>(dl[x], dh[x], cl[(x + 1) % 5], ch[(x + 1) % 5]);
+    uint32_t bl[5], bh[5];
+    krot<KECCAK_RHO[0]>(bl[0], bh[0], kxor3(al[0], cl[4], dl[0]), kxor3(ah[0], ch[4], dh[0]));
+    krot<KECCAK_RHO[6]>(bl[1], bh[1], kxor3(al[6], cl[0], dl[1]), kxor3(ah[6], ch[0], dh[1]));
+    krot<KECCAK_RHO[12]>(bl[2], bh[2], kxor3(al[12], cl[1], dl[2]), kxor3(ah[12], ch[1], dh[2]));
+    krot<KECCAK_RHO[18]>(bl[3], bh[3], kxor3(al[18], cl[2], dl[3]), kxor3(ah[18], ch[2], dh[3]));
+    krot<KECCAK_RHO[24]>(bl[4], bh[4], kxor3(al[24], cl[3], dl[4]), kxor3(ah[24], ch[3], dh[4]));
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+        al[x] = kchi(bl[x], bl[(x + 1) % 5], bl[(x + 2) % 5]);
+        ah[x] = kchi(bh[x], bh[(x + 1) % 5], bh[(x + 2) % 5]);
+    }
+    al[0] ^= (uint32_t)KECCAK_RC[23];
+    ah[0] ^= (uint32_t)(KECCAK_RC[23] >> 32);
+}
+
 GSV_DI void keccakf(uint64_t a[25]) {
     uint32_t al[25], ah[25];
 #pragma unroll
@@ -107,6 +141,19 @@ GSV_DI void keccakf(uint64_t a[25]) {
     keccakf_split(al, ah);
 #pragma unroll
     for (int k = 0; k < 25; k++) a[k] = (uint64_t)al[k] | ((uint64_t)ah[k] << 32);
+}
+
+// keccakf for a digest: only a[0..3] are defined afterwards
+GSV_DI void keccakf_digest(uint64_t a[25]) {
+    uint32_t al[25], ah[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) {
+        al[k] = (uint32_t)a[k];
+        ah[k] = (uint32_t)(a[k] >> 32);
+    }
+    keccakf_split_digest(al, ah);
+#pragma unroll
+    for (int k = 0; k < 4; k++) a[k] = (uint64_t)al[k] | ((uint64_t)ah[k] << 32);
 }
 
 // ---------------------------------------------------------------- group-cooperative Keccak-f
